@@ -1,0 +1,308 @@
+"""CPU ORACLE for the hot path -- TEST INFRASTRUCTURE ONLY.
+
+This is a PyTorch-CPU restatement of the reference's algorithms for the
+propagators and the DOE modulation.  It keeps the
+reference's operation sequence (centred ``fftshift`` grids, fully materialised
+transfer functions, per-call rebuild) so that it is both
+
+* the parity checker for the HIP kernels (``tests/``, ``__graft_entry__.smoke``), and
+* the ``cpu_baseline`` leg of ``bench.py`` (``kind: "port"``).
+
+It is never imported by the product package ``quantizationawarethzdoe_amd``.
+Parity status: PINNED -- ``tests/test_oracle_golden.py`` checks every function
+here against fixtures produced by running the reference itself
+(``tests/golden/gen_golden.py``): fp32 to <=1e-6 rel-L2 against the reference's
+fp32 outputs and fp64 to <=1e-12 against the reference's fp64 outputs.
+
+All functions take/return torch tensors; the working precision follows the
+input dtype (complex64 -> fp32 math, complex128 -> fp64 math).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+BASE_PLANE_THICKNESS = 2e-3  # Components/QuantizedDOE.py:23
+
+
+def _rdt(x: torch.Tensor) -> torch.dtype:
+    return torch.float64 if x.dtype in (torch.complex128, torch.float64) else torch.float32
+
+
+# ---------------------------------------------------------------------------------------------
+# ASM  (Props/ASM_Prop.py)
+# ---------------------------------------------------------------------------------------------
+def asm_padding(H: int, W: int, padding_scale, do_padding: bool = True):
+    """pad = floor(s*N/2), P = N + 2 pad  (Props/ASM_Prop.py:119-136)."""
+    if not do_padding:
+        return 0, 0, H, W
+    sh, sw = (padding_scale, padding_scale) if not isinstance(padding_scale, (list, tuple)) else padding_scale
+    ph = int(math.floor(float(sh) * H / 2))
+    pw = int(math.floor(float(sw) * W / 2))
+    return ph, pw, H + 2 * ph, W + 2 * pw
+
+
+def ft2(x):
+    """Centred ortho 2-D FFT (utils/Helper_Functions.py:99-160, core :150)."""
+    return torch.fft.fftshift(torch.fft.fft2(torch.fft.fftshift(x, dim=(-2, -1)), norm="ortho"), dim=(-2, -1))
+
+
+def ift2(x):
+    """Centred ortho inverse 2-D FFT (utils/Helper_Functions.py:111-160, ifftshift variant)."""
+    return torch.fft.ifftshift(torch.fft.ifft2(torch.fft.ifftshift(x, dim=(-2, -1)), norm="ortho"), dim=(-2, -1))
+
+
+def asm_transfer_function(Ph, Pw, wavelengths, dx, dy, z, bandlimit=True, bandlimit_type="exact", rdt=torch.float32):
+    """Band-limited ASM transfer function on the centred grid, [1, C, Ph, Pw].
+
+    Restates Props/ASM_Prop.py:138-145 (frequency grid: (i - P//2)/P, meshgrid 'ij'),
+    :245-262 (H = exp(i z sqrt(k^2 - K^2)), evanescent -> 0) and :288-306 (Matsushima
+    2009 band limits; note the reference uses the padded HEIGHT Ph for both axes,
+    :274-275 and :290-291).
+    """
+    kx = (torch.linspace(0, Ph - 1, Ph, dtype=rdt) - (Ph // 2)) / Ph
+    ky = (torch.linspace(0, Pw - 1, Pw, dtype=rdt) - (Pw // 2)) / Pw
+    KX, KY = torch.meshgrid(kx, ky, indexing="ij")
+    lam = wavelengths.to(rdt)[None, :, None, None]
+    dx = torch.as_tensor(dx, dtype=rdt)
+    dy = torch.as_tensor(dy, dtype=rdt)
+    z = torch.as_tensor(z, dtype=rdt)
+    Kx = 2 * math.pi * KX[None, None] / dx
+    Ky = 2 * math.pi * KY[None, None] / dy
+    K2 = Kx ** 2 + Ky ** 2
+    k = 2 * torch.tensor(math.pi, dtype=torch.float64) / lam
+    k2 = k ** 2
+    H = torch.exp(1j * (z * torch.sqrt(k2 - K2)))
+    H[(k2 - K2) < 0] = 0
+    if bandlimit:
+        du = ((2 * math.pi / dx) / (2 * Ph)) / (2 * math.pi)
+        dv = ((2 * math.pi / dy) / (2 * Ph)) / (2 * math.pi)
+        ulim = 1 / torch.sqrt((2 * du * z) ** 2 + 1) / lam
+        vlim = 1 / torch.sqrt((2 * dv * z) ** 2 + 1) / lam
+        if bandlimit_type == "exact":
+            c1 = ((Kx ** 2) / ((2 * math.pi * ulim) ** 2) + (Ky ** 2) / (k ** 2)) <= 1
+            c2 = ((Kx ** 2) / (k ** 2) + (Ky ** 2) / ((2 * math.pi * vlim) ** 2)) <= 1
+            H[~(c1 & c2)] = 0
+        elif bandlimit_type == "approx":
+            Lx = Ph * dx
+            Ly = Ph * dy
+            kxm = 2 * math.pi / torch.sqrt((2 * (1 / Lx) * z) ** 2 + 1) / lam
+            kym = 2 * math.pi / torch.sqrt((2 * (1 / Ly) * z) ** 2 + 1) / lam
+            H[(torch.abs(Kx) > kxm) | (torch.abs(Ky) > kym)] = 0
+        else:
+            raise Exception("Should not be in this state.")
+    return H
+
+
+def asm_critical_distance(Ph, dx, wavelengths):
+    """Zc = Ph dx^2 sqrt(1 - (lmax/2dx)^2) / lmax  (Props/ASM_Prop.py:280)."""
+    lmax = float(torch.max(torch.as_tensor(wavelengths)))
+    dx = float(dx)
+    return Ph * dx ** 2 * math.sqrt(1 - (lmax / (2 * dx)) ** 2) / lmax
+
+
+def asm_forward(data, wavelengths, spacing, z, padding_scale=1, do_padding=True, do_unpad_after_pad=True,
+                bandlimit=True, bandlimit_type="exact"):
+    """pad -> ft2 -> x H -> ift2 -> centre crop  (Props/ASM_Prop.py:314-378)."""
+    rdt = _rdt(data)
+    B, C, H, W = data.shape
+    ph, pw, Ph, Pw = asm_padding(H, W, padding_scale, do_padding)
+    x = torch.nn.functional.pad(data, (pw, pw, ph, ph)) if do_padding else data
+    Hf = asm_transfer_function(Ph, Pw, torch.as_tensor(wavelengths), spacing[0], spacing[1], z, bandlimit,
+                               bandlimit_type, rdt)
+    y = ift2(ft2(x) * Hf)
+    if do_padding and do_unpad_after_pad:
+        top = int(round((Ph - H) / 2.0))
+        left = int(round((Pw - W) / 2.0))
+        y = y[..., top:top + H, left:left + W]
+    return y
+
+
+# ---------------------------------------------------------------------------------------------
+# CZT  (Props/CZT_Prop.py)
+# ---------------------------------------------------------------------------------------------
+def _rs_kernel(z, mx, my, lam):
+    """exp(ikr) z/(2 pi r^2) (1/r - ik)  (Props/CZT_Prop.py:44-57)."""
+    k = 2 * torch.pi / lam[None, :, None, None]
+    r = torch.sqrt(mx ** 2 + my ** 2 + z ** 2)
+    return torch.exp(1j * k * r) * (1 / (2 * torch.pi) * z / r ** 2 * (1 / r - 1j * k))
+
+
+def _bluestein(x, f1, f2, Dm, M):
+    """One Bluestein pass along dim -2 with the reference's slicing (Props/CZT_Prop.py:132-225).
+
+    Output is the reference's transposed [.., n, M] layout with the off-by-one slice
+    ``[m : m+M]`` and post-chirp ``h[m-1 : m-1+M]`` (:211), then M_shift (:214-224).
+    """
+    _, _, m, n = x.shape
+    D1 = f1 + (M * Dm + f2 - f1) / (2 * M)
+    D2 = f2 + (M * Dm + f2 - f1) / (2 * M)
+    mp = m + M - 1
+    np2 = int(2 ** int(math.ceil(math.log2(mp))))
+    A = torch.exp(1j * 2 * torch.pi * D1 / Dm)
+    Wc = torch.exp(-1j * 2 * torch.pi * (D1 - D2) / (M * Dm))
+    jj = torch.arange(-m + 1, max(M - 1, m - 1) + 1)
+    h = Wc ** (jj ** 2 / 2)
+    ft = torch.fft.fft(1 / h[: mp + 1], n=np2, dim=-1)
+    pre = A ** (-(torch.arange(0, m))) * h[..., torch.arange(m - 1, 2 * m - 1)]
+    b = torch.fft.fft(x * torch.tile(pre, (1, 1, n, 1)).transpose(-2, -1), np2, dim=-2)
+    b = torch.fft.ifft(b * torch.tile(ft, (1, 1, n, 1)).transpose(-2, -1), dim=-2)
+    b = b[..., m:mp + 1, 0:n].transpose(-2, -1) * torch.tile(h[..., m - 1:mp], (1, 1, n, 1))
+    ell = torch.linspace(0, M - 1, M)[None, None, None, :]
+    ell = ell / M * (D2 - D1) + D1
+    shift = torch.tile(torch.exp(-1j * 2 * torch.pi * ell * (-m / 2 + 0.5) / Dm), (1, 1, n, 1))
+    return b * shift
+
+
+def czt_forward(data, wavelengths, spacing, z, outH=None, outW=None, odx=None, ody=None):
+    """Chirp-z (Bluestein) RS propagation  (Props/CZT_Prop.py:59-118, 227-314).
+
+    Runs in torch's current default float dtype for the grids (as the reference does);
+    callers set ``torch.set_default_dtype(torch.float64)`` for the fp64 oracle.
+    """
+    _, C, H, W = data.shape
+    dxi, dyi = spacing[0], spacing[1]
+    outH = H if outH is None else outH
+    outW = W if outW is None else outW
+    odx = dxi if odx is None else odx
+    ody = dyi if ody is None else ody
+    lam = torch.as_tensor(wavelengths)
+    z = torch.as_tensor(z)
+    xi = torch.linspace(-H * dxi / 2, H * dxi / 2, H)
+    yi = torch.linspace(-W * dyi / 2, W * dyi / 2, W)
+    imx, imy = torch.meshgrid(xi, yi, indexing="ij")
+    xo = torch.linspace(-outH * odx / 2, outH * odx / 2, outH)
+    yo = torch.linspace(-outW * ody / 2, outW * ody / 2, outW)
+    omx, omy = torch.meshgrid(xo, yo, indexing="ij")
+    Dm = lam[None, :, None, None] * z / dxi
+    fx1, fx2 = xo[0] + Dm / 2, xo[-1] + Dm / 2
+    fy1, fy2 = yo[0] + Dm / 2, yo[-1] + Dm / 2
+    F0 = _rs_kernel(z, omx, omy, lam)
+    F = _rs_kernel(z, imx, imy, lam)
+    U = data * F
+    U = _bluestein(U, fy1, fy2, Dm, outW)
+    U = _bluestein(U, fx1, fx2, Dm, outH)
+    return F0 * U * z * odx * ody * lam[None, :, None, None]
+
+
+# ---------------------------------------------------------------------------------------------
+# RSC  (Props/RSC_Prop.py)
+# ---------------------------------------------------------------------------------------------
+def rsc_forward(data, wavelengths, spacing, z):
+    """Rayleigh-Sommerfeld convolution on a 2N grid (Props/RSC_Prop.py:79-87, 129-215).
+
+    Grid: linspace(-P dx/2, P dx/2, P) on BOTH axes with dx (:83-84); B must be 1 (:198-200).
+    """
+    B, C, H, W = data.shape
+    dx, dy = spacing[0], spacing[1]
+    Ph, Pw = H + 2 * (H // 2), W + 2 * (W // 2)
+    lam = torch.as_tensor(wavelengths)
+    z = torch.as_tensor(z)
+    x = torch.linspace(-Ph * dx / 2, Ph * dx / 2, Ph)
+    y = torch.linspace(-Pw * dx / 2, Pw * dx / 2, Pw)
+    mx, my = torch.meshgrid(x, y, indexing="ij")
+    k = 2 * torch.pi / lam[:, None, None]
+    r = torch.sqrt(mx ** 2 + my ** 2 + z ** 2)
+    K = (torch.exp(1j * k * r) * (1 / (2 * torch.pi) * z / r ** 2 * (1 / r - 1j * k)))[None]
+    U = torch.zeros_like(K)
+    U[..., 0:H, 0:W] = data
+    S = torch.fft.fft2(U) * torch.fft.fft2(K) * dx * dy
+    return torch.fft.ifft2(S)[..., H:, W:]
+
+
+# ---------------------------------------------------------------------------------------------
+# DOE  (Components/QuantizedDOE.py)
+# ---------------------------------------------------------------------------------------------
+def doe_transmission(height, wavelengths, eps, tand):
+    """t_c(h) = exp(-k/2 (h+b) tand sqrt(eps)) exp(-i k (h+b)(sqrt(eps)-1))  (QuantizedDOE.py:47-79)."""
+    lam = torch.as_tensor(wavelengths).reshape(-1)[:, None, None]
+    k = 2 * torch.pi / lam
+    eps = torch.as_tensor(eps, dtype=height.dtype)
+    tand = torch.as_tensor(tand, dtype=height.dtype)
+    hb = height[None] + torch.tensor(BASE_PLANE_THICKNESS, dtype=height.dtype)
+    loss = torch.exp(-0.5 * k * hb * tand * torch.sqrt(eps))
+    delay = torch.exp(-1j * k * hb * (torch.sqrt(eps) - 1))
+    return loss * delay
+
+
+def doe_modulate(field, height, wavelengths, eps, tand, tolerance=None, noise_u01=None):
+    """add_height_map_noise -> nearest upsample -> x t  (QuantizedDOE.py:82-126).
+
+    ``noise_u01`` injects the ``rand_like`` draw (U[0,1)) the reference consumes at :85.
+    """
+    h = height
+    if tolerance is not None:
+        u = noise_u01 if noise_u01 is not None else torch.rand_like(h)
+        h = h + (u - 0.5) * 2 * tolerance
+    H, W = field.shape[-2:]
+    if h.shape[0] != H or h.shape[1] != W:
+        h = torch.nn.functional.interpolate(h[None, None], size=[H, W], mode="nearest")[0, 0]
+    return field * doe_transmission(h, wavelengths, eps, tand)[None]
+
+
+def copy_quad_to_full(q):
+    """Mirror a quadrant into the full map (QuantizedDOE.py:28-35), 2-D form."""
+    left = torch.cat([torch.flip(q, dims=[0]), q], dim=0)
+    return torch.cat([torch.flip(left, dims=[1]), left], dim=1)
+
+
+def height_to_phase(h, lam, n):
+    """QuantizedDOE.py:40-41."""
+    return 2 * torch.pi / lam * (n - 1) * h
+
+
+def sgv3_score(phase, phase_lut, s):
+    """score_phase(func='sigmoid')  (QuantizedDOE.py:794-817)."""
+    wp = (phase + torch.pi) % (2 * torch.pi) - torch.pi
+    lut = (phase_lut[None, :, None, None] + torch.pi) % (2 * torch.pi) - torch.pi
+    d = wp - lut
+    d = (d + torch.pi) % (2 * torch.pi) - torch.pi
+    d = d / torch.pi
+    zz = s * d
+    return torch.sigmoid(zz) * (1 - torch.sigmoid(zz)) * 4
+
+
+def sgv3_tau(iter_frac, tau_min, tau_max):
+    """Cosine temperature schedule (QuantizedDOE.py:869-871)."""
+    return tau_min + 0.5 * (tau_max - tau_min) * (1 + math.cos(iter_frac * math.pi))
+
+
+def sgv3_height_map(weight, lut, hmax, lam_min, eps, iter_frac, c_s, tau_max, tau_min, expo=None, num_unit=2):
+    """SoftGumbelQuantizedDOELayerv3.preprocessed_height_map  (QuantizedDOE.py:819-860).
+
+    ``expo`` injects the Exp(1) draw ``F.gumbel_softmax`` consumes (gumbel = -log(expo)).
+    Straight-through forward value: one-hot of argmax((s + g)/tau) over the level axis.
+    """
+    tau = sgv3_tau(iter_frac, tau_min, tau_max)
+    h = hmax * torch.sigmoid(torch.clamp(weight, min=-10.0, max=10.0))[None, None]
+    if iter_frac > 0.3:
+        n = torch.sqrt(torch.as_tensor(eps, dtype=weight.dtype))
+        plut = height_to_phase(lut, lam_min, n)
+        qph = height_to_phase(h, lam_min, n)
+        sc = sgv3_score(qph, plut, tau_max / tau) * c_s * (tau_max / tau)
+        g = -torch.log(expo) if expo is not None else -torch.empty_like(sc).exponential_().log()
+        y = torch.softmax((sc + g) / tau, dim=1)
+        idx = y.argmax(dim=1, keepdim=True)
+        onehot = torch.zeros_like(y).scatter_(1, idx, 1.0)
+        q = (lut.reshape(1, -1, 1, 1) * onehot).sum(1, keepdim=True)
+        if iter_frac <= 0.8:
+            beta = (iter_frac - 0.3) / (0.8 - 0.3)
+            h = (1 - beta) * h + beta * q
+        else:
+            h = q
+    h = h[0, 0]
+    return copy_quad_to_full(h) if num_unit is not None else h
+
+
+def ste_quantize(h, lut):
+    """Nearest-LUT level (first on ties), identity gradient (QuantizedDOE.py:1239-1255)."""
+    idx = torch.argmin(torch.abs(h.unsqueeze(-1) - lut), dim=-1)
+    return lut[idx]
+
+
+def normalize(x):
+    """Per-batch divide by max (utils/Helper_Functions.py:185-193), out of place."""
+    B = x.shape[0]
+    v = x.reshape(B, -1)
+    return (v / v.max(1, keepdim=True)[0]).reshape(x.shape)

@@ -1,0 +1,328 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE itself.
+
+Runs only in the build container (it imports /root/reference through
+``_refimport``; it refuses to run when the tree is absent).  Every case is run
+twice through the reference code:
+
+* ``out32`` -- the reference as shipped (fp32 spacing / wavelengths, complex64);
+* ``out64`` -- the same reference code in fp64 (default dtype float64, complex128
+  data, spacing and wavelengths set to ``.double()`` of the fp32-rounded values),
+  the procedure of SURVEY.md §8(c) "fp64 oracle".
+
+Inputs are seeded numpy draws; they are stored next to the outputs so the GPU
+tests never need the reference.  Usage::
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+"""
+import contextlib
+import io
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from _refimport import import_reference  # noqa: E402
+
+C0 = 2.998e8
+MM = 1e-3
+
+ref = import_reference()
+torch.set_num_threads(8)
+
+
+@contextlib.contextmanager
+def default_dtype(dt):
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dt)
+    try:
+        yield
+    finally:
+        torch.set_default_dtype(old)
+
+
+def quiet(fn, *a, **k):
+    """Run fn capturing the reference's diagnostic prints; return (result, text)."""
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        r = fn(*a, **k)
+    return r, buf.getvalue()
+
+
+def rand_field(shape, seed):
+    rng = np.random.default_rng(seed)
+    return (rng.standard_normal(shape) + 1j * rng.standard_normal(shape)).astype(np.complex64)
+
+
+def make_field(data_np, wavelengths, spacing, f64):
+    """ElectricField on CPU in fp32 (as shipped) or the fp64 procedure."""
+    if not f64:
+        return ref.ElectricField(data=torch.from_numpy(data_np.astype(np.complex64)),
+                                 wavelengths=wavelengths, spacing=spacing, device="cpu")
+    f = ref.ElectricField(data=torch.from_numpy(data_np.astype(np.complex128)),
+                          wavelengths=wavelengths, spacing=spacing, device="cpu")
+    f._wavelengths = f._wavelengths.double()
+    f._spacing = f._spacing.double()
+    return f
+
+
+def wl_arg(wl):
+    return wl if len(wl) > 1 else wl[0]
+
+
+# ----------------------------------------------------------------------------------------------
+# ASM (Props/ASM_Prop.py)
+# ----------------------------------------------------------------------------------------------
+ASM_CASES = [
+    # name, B, C(wavelength freqs GHz), H, W, dx, dy, z, padding_scale, bandlimit, type, do_padding, unpad
+    dict(name="n64_s1_exact", B=1, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.05, s=1, bl=True, t="exact"),
+    dict(name="n64_s1_2wl_z02", B=1, f=[280, 320], H=64, W=64, dx=0.5, dy=0.5, z=0.2, s=1, bl=True, t="exact"),
+    dict(name="n64_s15_approx", B=1, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.2, s=1.5, bl=True, t="approx"),
+    dict(name="n64_s2_negz", B=1, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=-0.05, s=2, bl=True, t="exact"),
+    dict(name="n64_s1_nobl", B=1, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.2, s=1, bl=False, t="exact"),
+    dict(name="n64_nopad", B=1, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.05, s=1, bl=True, t="exact",
+         do_padding=False),
+    dict(name="n64_keep_pad", B=1, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.05, s=1, bl=True, t="exact",
+         unpad=False),
+    dict(name="n64_b2", B=2, f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.1, s=1, bl=True, t="exact"),
+    dict(name="rect48x80", B=1, f=[300], H=48, W=80, dx=0.5, dy=0.75, z=0.1, s=1, bl=True, t="exact"),
+    dict(name="n100_s2_p300", B=1, f=[300], H=100, W=100, dx=1.0, dy=1.0, z=0.2, s=2, bl=True, t="exact"),
+    dict(name="n101_s1_p201", B=1, f=[300], H=101, W=101, dx=1.0, dy=1.0, z=0.05, s=1, bl=True, t="exact"),
+    dict(name="n101_s15_p251_2wl", B=1, f=[250, 330], H=101, W=101, dx=1.0, dy=1.0, z=0.2, s=1.5, bl=True,
+         t="approx"),
+    dict(name="n128_s1", B=1, f=[300], H=128, W=128, dx=0.5, dy=0.5, z=0.2, s=1, bl=True, t="exact"),
+]
+
+
+def run_asm(case, data_np, f64, grad_np=None):
+    wl = [C0 / (g * 1e9) for g in case["f"]]
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        field = make_field(data_np, wl_arg(wl), [case["dx"] * MM, case["dy"] * MM], f64)
+        prop = ref.ASM.ASM_prop(z_distance=case["z"], do_padding=case.get("do_padding", True),
+                                do_unpad_after_pad=case.get("unpad", True), padding_scale=case["s"],
+                                bandlimit_kernel=case["bl"], bandlimit_type=case["t"], device="cpu")
+        if grad_np is None:
+            out, txt = quiet(prop.forward, field)
+            return out.data.detach().numpy(), txt, None
+        field._data = field._data.clone().requires_grad_(True)
+        out, txt = quiet(prop.forward, field)
+        g = torch.from_numpy(grad_np.astype(np.complex128 if f64 else np.complex64))
+        (gin,) = torch.autograd.grad(out.data, field._data, grad_outputs=g)
+        return out.data.detach().numpy(), txt, gin.numpy()
+
+
+def gen_asm(manifest):
+    arrays = {}
+    for i, case in enumerate(ASM_CASES):
+        shape = (case["B"], len(case["f"]), case["H"], case["W"])
+        x = rand_field(shape, 1000 + i)
+        o32, txt, _ = run_asm(case, x, False)
+        want_grad = case["name"] in ("n64_s1_2wl_z02", "n100_s2_p300", "rect48x80")
+        g = rand_field(o32.shape, 5000 + i) if want_grad else None
+        o64, _, gi64 = run_asm(case, x, True, g)
+        k = case["name"]
+        arrays[f"{k}__in"] = x
+        arrays[f"{k}__out32"] = o32.astype(np.complex64)
+        arrays[f"{k}__out64"] = o64.astype(np.complex128)
+        if want_grad:
+            _, _, gi32 = run_asm(case, x, False, g)
+            arrays[f"{k}__gout"] = g
+            arrays[f"{k}__gin32"] = gi32.astype(np.complex64)
+            arrays[f"{k}__gin64"] = gi64.astype(np.complex128)
+        rel = np.linalg.norm(o32 - o64) / np.linalg.norm(o64)
+        manifest["asm"].append(dict(case, stdout=txt.strip(), rel32vs64=float(rel), grad=want_grad))
+        print(f"asm {k}: out {o32.shape} fp32-vs-fp64 rel {rel:.2e}")
+    np.savez_compressed(os.path.join(HERE, "asm_golden.npz"), **arrays)
+
+
+def gen_asm_cfg1(manifest):
+    """cfg1 checksum: ASM 1024^2 ones-field, z=0.2 m, dx=0.5 mm, 300 GHz, s=1, exact."""
+    case = dict(name="cfg1", B=1, f=[300], H=1024, W=1024, dx=0.5, dy=0.5, z=0.2, s=1, bl=True, t="exact")
+    x = np.ones((1, 1, 1024, 1024), np.complex64)
+    o32, txt, _ = run_asm(case, x, False)
+    o64, _, _ = run_asm(case, x, True)
+    arrs = dict(cfg1__sub32=o32[0, 0, ::32, ::32].astype(np.complex64),
+                cfg1__sub64=o64[0, 0, ::32, ::32].astype(np.complex128),
+                cfg1__row512_64=o64[0, 0, 512, :].astype(np.complex128))
+    np.savez_compressed(os.path.join(HERE, "asm_cfg1_golden.npz"), **arrs)
+    manifest["asm_cfg1"] = dict(case, stdout=txt.strip(),
+                                energy32=float(np.sum(np.abs(o32.astype(np.complex128)) ** 2)),
+                                energy64=float(np.sum(np.abs(o64) ** 2)),
+                                rel32vs64=float(np.linalg.norm(o32 - o64) / np.linalg.norm(o64)))
+    print("cfg1", manifest["asm_cfg1"]["energy32"], manifest["asm_cfg1"]["energy64"],
+          manifest["asm_cfg1"]["rel32vs64"])
+
+
+# ----------------------------------------------------------------------------------------------
+# CZT (Props/CZT_Prop.py) and RSC (Props/RSC_Prop.py)
+# ----------------------------------------------------------------------------------------------
+CZT_CASES = [
+    dict(name="czt64to16_2wl", B=1, f=[280, 320], H=64, W=64, dx=0.5, dy=0.5, z=0.1, oH=16, oW=16, odx=0.25,
+         ody=0.25),
+    dict(name="czt48x64to24", B=1, f=[300], H=48, W=64, dx=0.5, dy=0.5, z=0.15, oH=24, oW=24, odx=0.5, ody=0.5),
+    dict(name="czt_test_czt_200", B=1, f=[C0 / 1e-3 / 1e9], H=200, W=200, dx=1.0, dy=1.0, z=0.5, oH=200, oW=200,
+         odx=1.0, ody=1.0, gaussian=2.0),
+]
+
+
+def gaussian_input(case, f64):
+    """The reference's own Gaussian source (LightSource/Gaussian_beam.py:88-160), as test_czt.py uses it."""
+    wl = [C0 / (g * 1e9) for g in case["f"]]
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        gm = ref.GB.Guassian_beam(height=case["H"], width=case["W"], beam_waist_x=case["gaussian"] * MM,
+                                  beam_waist_y=case["gaussian"] * MM, wavelengths=wl_arg(wl), alpha=0,
+                                  spacing=case["dx"] * MM, device="cpu")
+        return gm().data.detach().numpy()
+
+
+def run_czt(case, data_np, f64):
+    wl = [C0 / (g * 1e9) for g in case["f"]]
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        field = make_field(data_np, wl_arg(wl), [case["dx"] * MM, case["dy"] * MM], f64)
+        prop = ref.CZT.CZT_prop(z_distance=case["z"], device="cpu")
+        out, txt = quiet(prop.forward, field, outputHeight=case["oH"], outputWidth=case["oW"],
+                         outputPixel_dx=case["odx"] * MM, outputPixel_dy=case["ody"] * MM)
+        return out.data.detach().numpy(), txt
+
+
+def run_rsc(case, data_np, f64):
+    wl = [C0 / (g * 1e9) for g in case["f"]]
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        field = make_field(data_np, wl_arg(wl), [case["dx"] * MM, case["dy"] * MM], f64)
+        prop = ref.RSC.RSC_prop(z_distance=case["z"], device="cpu")
+        out, txt = quiet(prop.forward, field)
+        return out.data.detach().numpy(), txt
+
+
+RSC_CASES = [
+    dict(name="rsc64", B=1, f=[C0 / 1e-3 / 1e9], H=64, W=64, dx=1.0, dy=1.0, z=0.3),
+    dict(name="rsc48x40_2wl", B=1, f=[250, 300], H=48, W=40, dx=1.0, dy=1.0, z=0.2),
+]
+
+
+def gen_czt_rsc(manifest):
+    arrays = {}
+    for i, case in enumerate(CZT_CASES):
+        shape = (case["B"], len(case["f"]), case["H"], case["W"])
+        x = gaussian_input(case, False).astype(np.complex64) if "gaussian" in case else rand_field(shape, 2000 + i)
+        o32, txt = run_czt(case, x, False)
+        o64, _ = run_czt(case, x, True)
+        k = case["name"]
+        arrays.update({f"{k}__in": x, f"{k}__out32": o32.astype(np.complex64),
+                       f"{k}__out64": o64.astype(np.complex128)})
+        rel = np.linalg.norm(o32 - o64) / np.linalg.norm(o64)
+        shapes = [l for l in txt.splitlines() if l.startswith("torch.Size")]
+        manifest["czt"].append(dict(case, rel32vs64=float(rel), printed_shapes=shapes))
+        print(f"czt {k}: out {o32.shape} rel {rel:.2e}")
+    np.savez_compressed(os.path.join(HERE, "czt_golden.npz"), **arrays)
+    arrays = {}
+    for i, case in enumerate(RSC_CASES):
+        shape = (case["B"], len(case["f"]), case["H"], case["W"])
+        x = rand_field(shape, 3000 + i)
+        o32, txt = run_rsc(case, x, False)
+        o64, _ = run_rsc(case, x, True)
+        k = case["name"]
+        arrays.update({f"{k}__in": x, f"{k}__out32": o32.astype(np.complex64),
+                       f"{k}__out64": o64.astype(np.complex128)})
+        rel = np.linalg.norm(o32 - o64) / np.linalg.norm(o64)
+        manifest["rsc"].append(dict(case, stdout=txt.strip(), rel32vs64=float(rel)))
+        print(f"rsc {k}: out {o32.shape} rel {rel:.2e}")
+    np.savez_compressed(os.path.join(HERE, "rsc_golden.npz"), **arrays)
+
+
+# ----------------------------------------------------------------------------------------------
+# DOE modulation + quantizers (Components/QuantizedDOE.py)
+# ----------------------------------------------------------------------------------------------
+EPS, TAND = 2.66, 0.03
+
+
+def gen_doe(manifest):
+    arrays = {}
+    # (1) FixDOEElement modulate, tolerance given, noise recorded; same-size and upsampled height maps.
+    for name, hshape, fshape, fr in [("fix_same", (64, 64), (2, 2, 64, 64), [280, 320]),
+                                     ("fix_upsample", (32, 48), (1, 1, 64, 96), [300])]:
+        rng = np.random.default_rng(7)
+        h = (rng.random(hshape) * 1e-3).astype(np.float32)
+        x = rand_field(fshape, 11)
+        wl = [C0 / (g * 1e9) for g in fr]
+        g = rand_field(fshape, 12)
+        for prec in (32, 64):
+            dt = torch.float64 if prec == 64 else torch.float32
+            with default_dtype(dt):
+                field = make_field(x, wl_arg(wl), [1 * MM, 1 * MM], prec == 64)
+                field._data = field._data.clone().requires_grad_(True)
+                doe = ref.DOE.FixDOEElement(height_map=h.astype(np.float64 if prec == 64 else np.float32),
+                                            tolerance=0.01 * MM, material=[EPS, TAND], device="cpu")
+                torch.manual_seed(99)
+                out = doe(field)
+                gg = torch.from_numpy(g.astype(np.complex128 if prec == 64 else np.complex64))
+                gx, gh = torch.autograd.grad(out.data, (field._data, doe.height_map), grad_outputs=gg)
+                torch.manual_seed(99)
+                noise = torch.rand(hshape)
+            arrays[f"{name}__out{prec}"] = out.data.detach().numpy()
+            arrays[f"{name}__gx{prec}"] = gx.numpy()
+            arrays[f"{name}__gh{prec}"] = gh.numpy()
+            arrays[f"{name}__noise{prec}"] = noise.numpy()
+        arrays[f"{name}__h"] = h
+        arrays[f"{name}__in"] = x
+        arrays[f"{name}__gout"] = g
+        manifest["doe"].append(dict(name=name, kind="FixDOEElement", hshape=hshape, fshape=fshape, f=fr,
+                                    tolerance=0.01 * MM, eps=EPS, tand=TAND, seed=99))
+        print("doe", name)
+    # (2) SoftGumbelQuantizedDOELayerv3 forward at three schedule phases, RNG draws recorded.
+    doe_params = dict(doe_size=[32, 32], doe_dxy=1 * MM, doe_level=4, num_unit=2,
+                      height_constraint_max=1 * MM, tolerance=0.01 * MM, material=[EPS, TAND])
+    optim_params = dict(c_s=100, tau_max=2.5, tau_min=1.5)
+    wl = C0 / 300e9
+    x = rand_field((1, 1, 32, 32), 21)
+    for iter_frac in (0.1, 0.5, 0.9):
+        name = f"sgv3_{iter_frac}"
+        torch.manual_seed(5)
+        layer = ref.DOE.SoftGumbelQuantizedDOELayerv3(doe_params, optim_params, device="cpu")
+        w = layer.weight_init_phase.detach().numpy().copy()
+        field = make_field(x, wl, [1 * MM, 1 * MM], False)
+        torch.manual_seed(77)
+        out = layer(field, iter_frac=iter_frac)
+        hmap = layer.height_map.detach().numpy().copy()
+        loss = (out.data.abs() ** 2).sum()
+        loss.backward()
+        gw = layer.weight_init_phase.grad.numpy().copy()
+        # replay the RNG stream exactly as the layer consumed it
+        torch.manual_seed(77)
+        expo = None
+        if iter_frac > 0.3:
+            expo = torch.empty((1, 4, 16, 16)).exponential_().numpy()
+        unif = torch.rand((32, 32)).numpy()
+        arrays.update({f"{name}__w": w, f"{name}__out32": out.data.detach().numpy(), f"{name}__hmap": hmap,
+                       f"{name}__gw": gw, f"{name}__unif": unif})
+        if expo is not None:
+            arrays[f"{name}__expo"] = expo
+        manifest["doe"].append(dict(name=name, kind="SoftGumbelQuantizedDOELayerv3", iter_frac=iter_frac,
+                                    doe_params=doe_params, optim_params=optim_params, wavelength=wl,
+                                    loss="sum |E|^2"))
+        print("doe", name, "levels", np.unique(np.round(hmap * 1e6)).size)
+    arrays["sgv3__in"] = x
+    np.savez_compressed(os.path.join(HERE, "doe_golden.npz"), **arrays)
+
+
+def main():
+    manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
+                "asm": [], "czt": [], "rsc": [], "doe": []}
+    gen_asm(manifest)
+    gen_asm_cfg1(manifest)
+    gen_czt_rsc(manifest)
+    gen_doe(manifest)
+    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+        json.dump(manifest, fh, indent=1, default=float)
+
+
+if __name__ == "__main__":
+    main()

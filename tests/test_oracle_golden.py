@@ -1,0 +1,161 @@
+"""Pin the CPU oracle (oracle/thz_oracle.py) to outputs of the reference itself.
+
+Fixtures come from tests/golden/gen_golden.py (the reference run in fp32 as shipped,
+and the same reference code in fp64).  CPU-only.
+"""
+import contextlib
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import thz_oracle as orc
+from tests.golden_io import arrays, manifest, rel_l2, spacing, wavelengths
+
+M = manifest()
+
+
+@contextlib.contextmanager
+def default_dtype(dt):
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(dt)
+    try:
+        yield
+    finally:
+        torch.set_default_dtype(old)
+
+
+def _asm(case, x, f64):
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        data = torch.from_numpy(x.astype(np.complex128 if f64 else np.complex64))
+        return orc.asm_forward(data, wavelengths(case["f"], f64), spacing(case["dx"], case["dy"], f64), case["z"],
+                               padding_scale=case["s"], do_padding=case.get("do_padding", True),
+                               do_unpad_after_pad=case.get("unpad", True), bandlimit=case["bl"],
+                               bandlimit_type=case["t"])
+
+
+@pytest.mark.parametrize("case", M["asm"], ids=[c["name"] for c in M["asm"]])
+def test_asm_oracle_matches_reference(case):
+    A = arrays("asm")
+    k = case["name"]
+    x = A[f"{k}__in"]
+    o32 = _asm(case, x, False).numpy()
+    o64 = _asm(case, x, True).numpy()
+    assert o32.shape == A[f"{k}__out32"].shape
+    assert rel_l2(o32, A[f"{k}__out32"]) <= 1e-6
+    assert rel_l2(o64, A[f"{k}__out64"]) <= 1e-12
+
+
+@pytest.mark.parametrize("case", [c for c in M["asm"] if c["grad"]], ids=lambda c: c["name"])
+def test_asm_oracle_adjoint_matches_reference_autograd(case):
+    """Backward of ASM == ASM at -z with identical masks, vs reference autograd."""
+    A = arrays("asm")
+    k = case["name"]
+    g = A[f"{k}__gout"]
+    with default_dtype(torch.float64):
+        gz = torch.from_numpy(g.astype(np.complex128))
+        # adjoint = conj(ASM(conj(g))) with the same transfer function: pad/crop transpose is crop/pad
+        B, C, H, W = gz.shape
+        ph, pw, Ph, Pw = orc.asm_padding(H, W, case["s"])
+        Hf = orc.asm_transfer_function(Ph, Pw, wavelengths(case["f"], True), *spacing(case["dx"], case["dy"], True),
+                                       case["z"], case["bl"], case["t"], torch.float64)
+        gp = torch.nn.functional.pad(gz, (pw, pw, ph, ph))
+        adj = orc.ift2(orc.ft2(gp.conj()) * Hf).conj().resolve_conj()[..., ph:ph + H, pw:pw + W]
+    assert rel_l2(adj.numpy(), A[f"{k}__gin64"]) <= 1e-12
+
+
+def test_asm_cfg1_checksum():
+    c = M["asm_cfg1"]
+    A = arrays("asm_cfg1")
+    with default_dtype(torch.float32):
+        x = torch.ones(1, 1, 1024, 1024, dtype=torch.complex64)
+        o = orc.asm_forward(x, wavelengths(c["f"]), spacing(c["dx"], c["dy"]), c["z"], 1, True, True, True, "exact")
+    e = float((o.abs().double() ** 2).sum())
+    assert abs(e - c["energy32"]) / c["energy32"] < 1e-6
+    assert rel_l2(o[0, 0, ::32, ::32].numpy(), A["cfg1__sub32"]) <= 1e-6
+
+
+def test_asm_zc_kat():
+    """Zc KAT 0.26003873 m: P=300, dx=1 mm, f=300 GHz (experiment_four_focal_spots.ipynb:279)."""
+    lam = float(wavelengths([300])[0])
+    assert abs(orc.asm_critical_distance(300, float(torch.tensor(1e-3, dtype=torch.float32)), lam) - 0.26003873) < 5e-7
+    # Zc 0.4333979 m at P=500 (experiment_extend_depth_of_focus.ipynb:385)
+    assert abs(orc.asm_critical_distance(500, float(torch.tensor(1e-3, dtype=torch.float32)), lam) - 0.4333979) < 5e-7
+
+
+def _czt(case, x, f64):
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        data = torch.from_numpy(x.astype(np.complex128 if f64 else np.complex64))
+        sp = spacing(case["dx"], case["dy"], f64)
+        od = spacing(case["odx"], case["ody"], f64)
+        return orc.czt_forward(data, wavelengths(case["f"], f64), sp, case["z"], case["oH"], case["oW"],
+                               float(od[0]) if not f64 else case["odx"] * 1e-3,
+                               float(od[1]) if not f64 else case["ody"] * 1e-3)
+
+
+@pytest.mark.parametrize("case", M["czt"], ids=[c["name"] for c in M["czt"]])
+def test_czt_oracle_matches_reference(case):
+    A = arrays("czt")
+    k = case["name"]
+    x = A[f"{k}__in"]
+    o32 = _czt(case, x, False).numpy()
+    o64 = _czt(case, x, True).numpy()
+    assert o32.shape == A[f"{k}__out32"].shape
+    assert rel_l2(o32, A[f"{k}__out32"]) <= 1e-5
+    assert rel_l2(o64, A[f"{k}__out64"]) <= 1e-10
+
+
+@pytest.mark.parametrize("case", M["rsc"], ids=[c["name"] for c in M["rsc"]])
+def test_rsc_oracle_matches_reference(case):
+    A = arrays("rsc")
+    k = case["name"]
+    x = A[f"{k}__in"]
+    for f64 in (False, True):
+        dt = torch.float64 if f64 else torch.float32
+        with default_dtype(dt):
+            data = torch.from_numpy(x.astype(np.complex128 if f64 else np.complex64))
+            o = orc.rsc_forward(data, wavelengths(case["f"], f64), spacing(case["dx"], case["dy"], f64),
+                                case["z"]).numpy()
+        ref = A[f"{k}__out64" if f64 else f"{k}__out32"]
+        assert rel_l2(o, ref) <= (1e-12 if f64 else 1e-6)
+
+
+@pytest.mark.parametrize("name", ["fix_same", "fix_upsample"])
+def test_doe_modulate_oracle_matches_reference(name):
+    A = arrays("doe")
+    case = [c for c in M["doe"] if c["name"] == name][0]
+    for prec in (32, 64):
+        dt = torch.float64 if prec == 64 else torch.float32
+        cdt = torch.complex128 if prec == 64 else torch.complex64
+        with default_dtype(dt):
+            h = torch.from_numpy(A[f"{name}__h"].astype(np.float64 if prec == 64 else np.float32))
+            x = torch.from_numpy(A[f"{name}__in"]).to(cdt)
+            u = torch.from_numpy(A[f"{name}__noise{prec}"])
+            eps = torch.tensor([case["eps"], case["tand"]])
+            o = orc.doe_modulate(x, h, wavelengths(case["f"], prec == 64), eps[0], eps[1],
+                                 tolerance=torch.tensor(case["tolerance"]), noise_u01=u)
+        assert rel_l2(o.numpy(), A[f"{name}__out{prec}"]) <= (1e-12 if prec == 64 else 1e-6)
+
+
+@pytest.mark.parametrize("iter_frac", [0.1, 0.5, 0.9])
+def test_sgv3_height_map_oracle_matches_reference(iter_frac):
+    A = arrays("doe")
+    name = f"sgv3_{iter_frac}"
+    case = [c for c in M["doe"] if c["name"] == name][0]
+    dp, op = case["doe_params"], case["optim_params"]
+    w = torch.from_numpy(A[f"{name}__w"])
+    lut = torch.linspace(0, torch.tensor(dp["height_constraint_max"]), dp["doe_level"] + 1)[:-1]
+    expo = torch.from_numpy(A[f"{name}__expo"]) if f"{name}__expo" in A else None
+    lam = torch.tensor([case["wavelength"]], dtype=torch.float32)
+    h = orc.sgv3_height_map(w, lut, torch.tensor(dp["height_constraint_max"]), lam.min(),
+                            torch.tensor(dp["material"])[0], iter_frac, op["c_s"], op["tau_max"], op["tau_min"],
+                            expo=expo, num_unit=dp["num_unit"])
+    np.testing.assert_array_equal(h.numpy(), A[f"{name}__hmap"])
+
+
+def test_ste_kat():
+    """STE KAT: [0.1,0.4,0.7,1.2] on LUT [0,.5,1] -> [0,.5,.5,1] (Components/test_all.ipynb:595-606)."""
+    q = orc.ste_quantize(torch.tensor([0.1, 0.4, 0.7, 1.2]), torch.tensor([0.0, 0.5, 1.0]))
+    assert q.tolist() == [0.0, 0.5, 0.5, 1.0]
