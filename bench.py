@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Headline benchmark: complex-field propagations/s (N x N) + achieved HBM GB/s.
+
+Workload (BASELINE.json configs[1]): band-limited ASM of a 4096^2
+Gaussian beam (w = 50 mm, 300 GHz, dx = 0.25 mm, padding_scale 1 -> P = 8192, exact
+band limit) to 64 z-planes per GPU, z spread over 20..120 mm (the extend-DOF sweep,
+experiment_extend_depth_of_focus.ipynb:229).  One step = all 64 planes of one rank
+through the hand-written gfx950 kernels (one shared row pass + per-z column / row
+passes).  Multi-GPU: one process per GPU, z-planes sharded across ranks (weak
+scaling: 64 planes per rank, the global sweep grows with N), no data-path collective;
+a barrier + synchronize bracket the timed region and the max time over ranks counts.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+C0 = 2.998e8
+N_FIELD = 4096
+DX = 0.25e-3
+WAIST = 50e-3
+FREQ = 300e9
+Z_PER_RANK = 64
+Z_MIN, Z_MAX = 20e-3, 120e-3
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+METRIC = "complex-field propagations/sec (N×N) + achieved HBM GB/s at 1/2/4/8 GPU"
+
+
+def gaussian(N, dx, w, device):
+    """Gaussian_beam (LightSource/Gaussian_beam.py:88-160) at its waist (z_w0 = 0, R = 1e12):
+    amplitude exp(-(x^2+y^2)/w^2); the 1e12 m curvature phase (< 1e-8 rad) is dropped."""
+    xs = torch.linspace(-dx * N / 2, dx * N / 2, N, device=device, dtype=torch.float32)
+    X, Y = torch.meshgrid(xs, xs, indexing="ij")
+    return torch.exp(-(X * X) / (w * w) - (Y * Y) / (w * w)).to(torch.complex64)[None, None]
+
+
+def z_planes(rank, world):
+    total = Z_PER_RANK * world
+    zs = torch.linspace(Z_MIN, Z_MAX, total, dtype=torch.float64)
+    return [float(v) for v in zs[rank * Z_PER_RANK:(rank + 1) * Z_PER_RANK]]
+
+
+def cpu_baseline(budget_s=12.0, max_planes=8):
+    """The oracle (PyTorch-CPU restatement of the reference op sequence, oracle/thz_oracle.py)
+    timed on this host's cores on a bounded sample of the same workload (whole 4096^2 planes)."""
+    from oracle import thz_oracle as orc
+    threads = torch.get_num_threads()
+    x = gaussian(N_FIELD, DX, WAIST, "cpu")
+    lam = torch.tensor([C0 / FREQ], dtype=torch.float32)
+    sp = torch.tensor([DX, DX], dtype=torch.float32)
+    zs = z_planes(0, 1)
+    orc.asm_forward(x[..., :512, :512], lam, sp, zs[0], 1)  # warm MKL
+    t0 = time.perf_counter()
+    n = 0
+    while n < max_planes:
+        orc.asm_forward(x, lam, sp, zs[n % len(zs)], 1)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "propagations/s", "cores": threads, "kind": "port",
+            "sample": f"{n} planes of the cfg2 workload (4096^2 -> P=8192, exact band limit) through "
+                      f"oracle.thz_oracle.asm_forward, torch-CPU fp32, {threads} threads, {dt:.1f} s"}
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as fh:
+            return json.load(fh)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--z-chunk", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from quantizationawarethzdoe_amd import _lib
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_band_columns
+
+    x = gaussian(N_FIELD, DX, WAIST, dev)
+    zs = z_planes(rank, world)
+    lam = [float(torch.tensor(C0 / FREQ, dtype=torch.float32))]
+    sp = [float(torch.tensor(DX, dtype=torch.float32))] * 2
+    pad = N_FIELD // 2
+    out = torch.empty((len(zs), 1, 1, N_FIELD, N_FIELD), dtype=torch.complex64, device=dev)
+
+    def step():
+        asm_apply(x, lam, sp, zs, pad, pad, True, 1, z_chunk=args.z_chunk, out=out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _lib.timing_enable(False)
+    kern = {k: _lib.timing_read(k) for k in ("asm_rows_fwd", "asm_cols", "asm_rows_inv")}
+    if dist is not None:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    planes = Z_PER_RANK * world * args.steps
+    value = planes / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # algorithmic bytes per launch (SURVEY §8(d) byte model, pruned to the kept spectral band)
+    ncols = asm_band_columns(1, 1, N_FIELD, N_FIELD, pad, pad, True, 1, lam, sp, zs)
+    H = W = N_FIELD
+    nz = len(zs) if args.z_chunk == 0 else args.z_chunk
+    from quantizationawarethzdoe_amd.propagation import _asm_desc  # noqa: F401
+    bytes_rows_fwd = 8 * (H * W + ncols * H)
+    per_launch = {
+        "asm_rows_fwd": bytes_rows_fwd,
+    }
+    # chunking: the library default keeps U <= 128 MiB, i.e. z_chunk = floor(128 MiB / (ncols*H*8))
+    zc = args.z_chunk or max(1, int((128 * 1024 * 1024) // (ncols * H * 8)))
+    zc = min(zc, len(zs))
+    per_launch["asm_cols"] = 8 * (ncols * H + zc * ncols * H)
+    per_launch["asm_rows_inv"] = 8 * (zc * ncols * H + zc * H * W)
+    stats = {}
+    for k, (ms, n) in kern.items():
+        if n:
+            avg = ms / n
+            stats[k] = {"avg_ms": avg, "launches": n, "alg_bytes": per_launch[k],
+                        "gbs": per_launch[k] / (avg * 1e-3) / 1e9}
+    dom = max(stats, key=lambda k: stats[k]["avg_ms"] * stats[k]["launches"]) if stats else None
+    total_alg = sum(per_launch[k] * stats[k]["launches"] for k in stats) / args.steps
+    traffic = load_traffic()
+    roof = None
+    if dom:
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(stats[dom]["gbs"], 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(stats[dom]["gbs"] / HBM_PEAK_GBS, 4),
+                "traffic": (traffic or {}).get(dom),
+                "alg_bytes_per_launch": per_launch[dom], "avg_launch_ms": round(stats[dom]["avg_ms"], 4)}
+
+    line = {
+        "metric": METRIC, "value": round(value, 2), "unit": "propagations/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "complex64 (fp32)",
+        "data": "synthetic (Gaussian beam generated on device)",
+        "config": {"workload": "cfg2: ASM_prop 4096x4096 Gaussian_beam -> 64 z-planes/GPU (20-120 mm), "
+                               "300 GHz, dx 0.25 mm, padding_scale 1 (P=8192), exact band limit",
+                   "planes_per_step_per_gpu": Z_PER_RANK, "N": N_FIELD, "P": 2 * N_FIELD,
+                   "band_columns": ncols, "parallelism": f"z-shard x{world}"},
+        "hbm_gbs_algorithmic": round(total_alg * args.steps / elapsed / 1e9 * world, 1),
+        "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                    for k, v in stats.items()},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+"""Band-limited angular-spectrum propagator, ASM_prop -- drop-in for Props/ASM_Prop.py.
+
+Same constructor (``z_distance, do_padding, do_unpad_after_pad, padding_scale,
+bandlimit_kernel, bandlimit_type, device``; Props/ASM_Prop.py:19-117), same
+``padding_scale`` validation and ``Exception`` text (:75-98), same ``z`` property
+(:185-195, including that assigning a non-tensor stores the raw value), same
+once-per-instance critical-distance diagnostic (:279-285), same ``forward(field) ->
+ElectricField`` (:314-378) and the same OOM hint on ``RuntimeError`` (:363-370).
+
+The math runs in libthzdoe's hand-written gfx950 kernels (thz_asm.hip); the
+transfer function is never materialised.  Backward is the adjoint kernel.
+MI355X addition (opt-in, additive): ``propagate_planes(field, z_list)`` evaluates
+many z-planes with one shared forward row pass (the extend-DOF sweep of
+experiment_extend_depth_of_focus.ipynb:229-256) and returns [Z, B, C, H, W].
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+from quantizationawarethzdoe_amd import propagation as _prop
+
+
+def _z_host(z):
+    if torch.is_tensor(z):
+        return [float(v) for v in z.detach().reshape(-1).cpu().tolist()]
+    if isinstance(z, (list, tuple, np.ndarray)):
+        return [float(v) for v in np.asarray(z).reshape(-1)]
+    return [float(z)]
+
+
+class ASM_prop(nn.Module):
+    def __init__(self, z_distance: float = 0.0, do_padding: bool = True, do_unpad_after_pad: bool = True,
+                 padding_scale=None, bandlimit_kernel: bool = True, bandlimit_type: str = "exact",
+                 device: str = None) -> None:
+        super().__init__()
+        DEFAULT_PADDING_SCALE = torch.tensor([1, 1])
+        if do_padding:
+            err = False
+            if not torch.is_tensor(padding_scale):
+                if padding_scale is None:
+                    padding_scale = DEFAULT_PADDING_SCALE
+                elif np.isscalar(padding_scale):
+                    padding_scale = torch.tensor([padding_scale, padding_scale])
+                else:
+                    padding_scale = torch.tensor(padding_scale)
+                    if padding_scale.numel() != 2:
+                        err = True
+            elif padding_scale.numel() == 1:
+                padding_scale = padding_scale.squeeze()
+                padding_scale = torch.tensor([padding_scale, padding_scale])
+            elif padding_scale.numel() == 2:
+                padding_scale = padding_scale.squeeze()
+            else:
+                err = True
+            if err:
+                raise Exception("Invalid value for argument 'padding_scale'.  Should be a real-valued non-negative "
+                                "scalar number or a two-element tuple/tensor containing real-valued non-negative "
+                                "scalar numbers.")
+        else:
+            padding_scale = None
+        self.device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        self._z = torch.tensor(z_distance, device=self.device)
+        self._zh = _z_host(z_distance)
+        self.do_padding = do_padding
+        self.do_unpad_after_pad = do_unpad_after_pad
+        self.padding_scale = padding_scale
+        self.bandlimit_kernel = bandlimit_kernel
+        self.bandlimit_type = bandlimit_type
+        if bandlimit_kernel and bandlimit_type not in ("exact", "approx"):
+            self._bad_type = True
+        self.shape = None
+        self.check_Zc = True
+
+    # -- z property (Props/ASM_Prop.py:185-195) -----------------------------------------------
+    @property
+    def z(self):
+        return self._z
+
+    @z.setter
+    def z(self, z) -> None:
+        if isinstance(z, torch.Tensor) and z.device != torch.device(self.device):
+            z = z.to(self.device)
+        self._z = z
+        self._zh = _z_host(z)
+
+    def compute_padding(self, H, W, return_size_of_padding=False):
+        """Props/ASM_Prop.py:119-136."""
+        if not self.do_padding:
+            ph, pw = 0, 0
+        else:
+            ph = int(np.floor((float(self.padding_scale[0]) * H) / 2))
+            pw = int(np.floor((float(self.padding_scale[1]) * W) / 2))
+        if return_size_of_padding:
+            return ph, pw
+        return H + 2 * ph, W + 2 * pw
+
+    def _bandlimit_code(self):
+        if not self.bandlimit_kernel:
+            return 0
+        if self.bandlimit_type == "exact":
+            return 1
+        if self.bandlimit_type == "approx":
+            return 2
+        raise Exception("Should not be in this state.")
+
+    def _zc_diagnostic(self, Ph, dx, wavelengths_host, z):
+        """Critical distance print, once per instance (Props/ASM_Prop.py:279-285)."""
+        if not (self.bandlimit_kernel and self.check_Zc):
+            return
+        lmax = np.float32(max(wavelengths_host))
+        dx = np.array([dx], dtype=np.float32)
+        zc = (np.float32(Ph) * dx ** 2) * np.sqrt(np.float32(1) - (lmax / (np.float32(2) * dx)) ** 2) / lmax
+        if z > zc[0]:
+            print("The propagation distance is greater than critical distance {} m, the TF will be undersampled!"
+                  .format(zc))
+        else:
+            print("The critical distance is {} m, the TF will be fine during the sampling !".format(zc))
+        self.check_Zc = False
+
+    def _run(self, field: ElectricField, zs):
+        data = field.data
+        B, C, H, W = data.shape
+        ph, pw = self.compute_padding(H, W, return_size_of_padding=True)
+        bl = self._bandlimit_code()
+        wl = field.wavelengths_host
+        sp = field.spacing_host
+        self._zc_diagnostic(H + 2 * ph, sp[0], wl, zs[0])
+        cdt = data.dtype
+        x = data if cdt == torch.complex64 else data.to(torch.complex64)
+        try:
+            out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=(not self.do_padding) or self.do_unpad_after_pad,
+                                      bandlimit=bl)
+        except RuntimeError as err:
+            print("##################################################")
+            print("An error occurred.  If the error was due to insufficient memory, try decreasing the size of the "
+                  "input field or the size of the padding (i.e. decrease 'padding_scale').")
+            print("For the best results (e.g. to avoid convolution edge artifacts), the support of the input field "
+                  "should be at most 1/2 the size of the input field after padding.")
+            print("##################################################")
+            raise err
+        return out if cdt == torch.complex64 else out.to(cdt)
+
+    def forward(self, field: ElectricField) -> ElectricField:
+        """pad -> ft2 -> x H -> ift2 -> crop (Props/ASM_Prop.py:314-378), on the MI355X kernels."""
+        out = self._run(field, self._zh[:1])
+        Eout = ElectricField(data=out[0], wavelengths=field.wavelengths, spacing=field.spacing, device=field.device)
+        return Eout._adopt_host(field)
+
+    def propagate_planes(self, field: ElectricField, z_list) -> torch.Tensor:
+        """Additive API: all planes of ``z_list`` in one call -> [Z, B, C, Ho, Wo]."""
+        zs = _z_host(z_list)
+        outs = []
+        for k in range(0, len(zs), _prop._lib.THZ_MAX_Z):
+            outs.append(self._run(field, zs[k:k + _prop._lib.THZ_MAX_Z]))
+        return outs[0] if len(outs) == 1 else torch.cat(outs, 0)

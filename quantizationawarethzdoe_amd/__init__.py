@@ -1,0 +1,23 @@
+"""MI355X-native hot path of QuantizationAwareTHzDOE.
+
+Sub-packages mirror the reference's module paths (``DataType``, ``Props``,
+``Components``, ``LightSource``, ``utils``) so the reference's notebooks can import
+this framework unchanged after ``install_reference_aliases()``; the math runs in
+the hand-written gfx950 kernels of ``libthzdoe.so`` (``csrc/``) via ``_lib``.
+"""
+import importlib
+import sys
+
+__version__ = "0.1.0"
+
+_ALIASES = ("DataType", "Props", "Components", "LightSource", "utils")
+
+
+def install_reference_aliases():
+    """Make ``from Props.ASM_Prop import ASM_prop`` (the reference's import paths) resolve here."""
+    for name in _ALIASES:
+        mod = importlib.import_module(f"{__name__}.{name}")
+        sys.modules[name] = mod
+        for sub in list(sys.modules):
+            if sub.startswith(f"{__name__}.{name}."):
+                sys.modules[sub[len(__name__) + 1:]] = sys.modules[sub]

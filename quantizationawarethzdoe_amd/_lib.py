@@ -1,0 +1,114 @@
+"""ctypes binding of libthzdoe.so (include/thzdoe.h).
+
+The shared library is built in-tree by ``quantizationawarethzdoe_amd/csrc/Makefile``
+(``__graft_entry__.build()``).  There is NO fallback: if the library is missing or a
+symbol is absent, every product entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("THZDOE_LIB", os.path.join(_HERE, "libthzdoe.so"))
+
+THZ_OK = 0
+THZ_E_ARG = 1
+THZ_E_UNSUPPORTED = 2
+THZ_E_WORKSPACE = 3
+THZ_E_HIP = 4
+THZ_MAX_WAVELENGTHS = 64
+THZ_MAX_Z = 256
+
+BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
+
+# every symbol include/thzdoe.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "thz_version", "thz_last_error",
+    "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band",
+    "thz_fft_rows",
+    "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
+]
+
+
+class ThzError(RuntimeError):
+    """A libthzdoe call failed; carries the THZ_E_* code."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libthzdoe error {code}: {msg}")
+        self.code = code
+
+
+class AsmDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("pad_h", ctypes.c_int), ("pad_w", ctypes.c_int),
+        ("unpad", ctypes.c_int), ("bandlimit", ctypes.c_int), ("Z", ctypes.c_int),
+        ("adjoint", ctypes.c_int), ("z_chunk", ctypes.c_int),
+        ("dx", ctypes.c_float), ("dy", ctypes.c_float),
+        ("wavelengths", ctypes.POINTER(ctypes.c_float)), ("z", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(lib):
+    c_int, c_void_p, c_size_t = ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t
+    lib.thz_version.restype = ctypes.c_char_p
+    lib.thz_last_error.restype = ctypes.c_char_p
+    lib.thz_asm_workspace_size.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_size_t)]
+    lib.thz_asm_forward.argtypes = [ctypes.POINTER(AsmDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.thz_asm_band.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_int)]
+    lib.thz_fft_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+    lib.thz_timing_enable.argtypes = [c_int]
+    lib.thz_timing_reset.argtypes = []
+    lib.thz_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
+    for name in EXPORTED[2:]:
+        getattr(lib, name).restype = c_int
+
+
+def lib():
+    """Load (once) and return the ctypes handle; raise loudly if it cannot be loaded."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ThzError(-1, f"{LIB_PATH} not built: run __graft_entry__.build() "
+                                       "(make -C quantizationawarethzdoe_amd/csrc)")
+                h = ctypes.CDLL(LIB_PATH)
+                _declare(h)
+                _lib = h
+    return _lib
+
+
+def check(code):
+    if code != THZ_OK:
+        raise ThzError(code, lib().thz_last_error().decode())
+
+
+def version():
+    return lib().thz_version().decode()
+
+
+def timing_enable(on=True):
+    check(lib().thz_timing_enable(int(bool(on))))
+
+
+def timing_reset():
+    check(lib().thz_timing_reset())
+
+
+def timing_read(kernel):
+    """(total_ms, launches) of one kernel since the last reset; synchronises pending events."""
+    ms, n = ctypes.c_double(0), ctypes.c_long(0)
+    check(lib().thz_timing_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value
+
+
+def float_array(values):
+    arr = (ctypes.c_float * max(1, len(values)))(*[float(v) for v in values])
+    return arr

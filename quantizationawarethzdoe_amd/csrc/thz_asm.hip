@@ -1,0 +1,502 @@
+// Band-limited angular-spectrum propagation (Props/ASM_Prop.py:17-378) for gfx950.
+//
+// The reference computes crop(ift2(ft2(pad x) * H_centred)).  The four fftshifts cancel
+// against the centred grid, so this is crop(IFFT2(FFT2(pad x) * H_nat))
+// with H evaluated on the natural (fftfreq) index order.  It runs as three LDS passes
+// with NO materialised padding, transfer function or shifts:
+//
+//   K1 rows_fwd  : per input row, length-Pw FFT of the zero-padded row; keep only the
+//                  spectral column band |m_y| <= J that can be non-zero (evanescent and
+//                  band-limit cut-offs, computed on the host), store column-major
+//                  T[bc][c][h] so the column pass reads contiguous memory.
+//   K2 cols      : per (bc, band column c): length-Ph FFT of the zero-padded column,
+//                  then for each z of the chunk: x H_z(kx, ky) evaluated on the fly
+//                  (fp32, same operation order as the reference, contraction off),
+//                  inverse FFT, keep the Ho cropped rows, scale 1/(Ph Pw).  The spectrum
+//                  is kept in registers across the z loop (forward FFT once per column).
+//   K3 rows_inv  : per output row, gather the band (zero elsewhere), length-Pw inverse
+//                  FFT, keep the Wo cropped columns, write out[z][b][c][h][w].
+//
+// The adjoint (autograd backward) is the same pipeline with conj(H) and the input and
+// output windows exchanged.
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+#include <vector>
+
+#include "thz_common.hpp"
+
+namespace thz {
+
+constexpr float TWO_PI_F = 6.283185307179586f;  // (float)(2*pi), as torch casts the python scalar
+
+struct AsmArgs {
+  int BC, C;
+  int Ph, Pw;
+  int in_r0, in_c0, Hin, Win;     // input window inside the padded plane
+  int out_r0, out_c0, Hout, Wout; // output window
+  int ncols, J;                   // kept spectral columns, m_y = c - J
+  int nz, zoff;                   // z-planes in this chunk, offset into zv
+  int bl, adjoint;
+  float dx, dy, scale;
+  float lam[THZ_MAX_WAVELENGTHS];
+  float zv[THZ_MAX_Z];
+};
+
+// Blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch).  Map each run
+// of 16 consecutive rows (one 128-B line of a column-major T/U column) onto one XCD so
+// the strided 8-B accesses of K1/K3 combine in that XCD's L2.  Speed only.
+__device__ __forceinline__ int xcd_rows(int b, int nb) {
+  if (nb & 127) return b;
+  const int xcd = b & 7, slot = b >> 3;
+  return (((slot >> 4) << 3) + xcd) * 16 + (slot & 15);
+}
+
+__device__ __forceinline__ int freq_index(int i, int n) { return i < n - n / 2 ? i : i - n; }
+
+// Per-(wavelength, z) scalars of the transfer function, fp32 with the reference's
+// operation order (Props/ASM_Prop.py:253, 290-294, 303-304).
+struct TfScalars {
+  float z, kl2, A, Bv, kxm, kym;
+};
+
+#pragma clang fp contract(off)
+__device__ __forceinline__ TfScalars tf_scalars(const AsmArgs& a, float lam, float z) {
+  TfScalars s;
+  s.z = z;
+  const float kl = TWO_PI_F / lam;
+  s.kl2 = kl * kl;
+  const float du = ((TWO_PI_F / a.dx) / (float)(2 * a.Ph)) / TWO_PI_F;
+  const float dv = ((TWO_PI_F / a.dy) / (float)(2 * a.Ph)) / TWO_PI_F;  // Ph for v too (:291)
+  const float tu = (2.0f * du) * z;
+  const float tv = (2.0f * dv) * z;
+  const float ul = (1.0f / sqrtf(tu * tu + 1.0f)) / lam;
+  const float vl = (1.0f / sqrtf(tv * tv + 1.0f)) / lam;
+  const float au = TWO_PI_F * ul, av = TWO_PI_F * vl;
+  s.A = au * au;
+  s.Bv = av * av;
+  const float lx = (float)a.Ph * a.dx, ly = (float)a.Ph * a.dy;  // length_y uses Ph (:275)
+  const float ax = (2.0f * (1.0f / lx)) * z, ay = (2.0f * (1.0f / ly)) * z;
+  s.kxm = (TWO_PI_F / sqrtf(ax * ax + 1.0f)) / lam;
+  s.kym = (TWO_PI_F / sqrtf(ay * ay + 1.0f)) / lam;
+  return s;
+}
+
+// sin/cos of a float angle (|ang| up to ~1e5 rad): 3-constant Cody-Waite reduction by pi/2
+// (exact for the quadrant counts reached here), then minimax polynomials on [-pi/4, pi/4].
+// ~1 ulp, a few registers -- ocml's large-argument sincosf path is avoided because it
+// triples the register footprint of the column kernel.
+__device__ __forceinline__ void sincos_rad(float ang, float* sn, float* cs) {
+  const float q = rintf(ang * 0.636619772367581343f);
+  float r = fmaf(-q, 1.5707963705062866f, ang);
+  r = fmaf(-q, -4.3711388286737929e-08f, r);
+  r = fmaf(-q, -1.7151245100059206e-15f, r);
+  const float r2 = r * r;
+  // sin(r) ~ r + r^3 (s1 + r^2 (s2 + r^2 s3)),  cos(r) ~ 1 + r^2 (c1 + r^2 (c2 + r^2 (c3 + r^2 c4)))
+  float ps = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+  ps = fmaf(r2, ps, -1.6666654611e-1f);
+  const float sr = fmaf(r * r2, ps, r);
+  float pc = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+  pc = fmaf(r2, pc, 4.166664568298827e-2f);
+  pc = fmaf(r2, pc, -0.5f);
+  const float cr = fmaf(r2, pc, 1.0f);
+  const int iq = (int)q;
+  const bool swap = iq & 1;
+  float s0 = swap ? cr : sr;
+  float c0 = swap ? sr : cr;
+  if (iq & 2) s0 = -s0;
+  if ((iq + 1) & 2) c0 = -c0;
+  *sn = s0;
+  *cs = c0;
+}
+
+__device__ __forceinline__ float kfreq(int m, int P, float d) { return (TWO_PI_F * ((float)m / (float)P)) / d; }
+
+// H(kx, ky) = exp(i z sqrt(k^2 - K^2)) with the evanescent and band-limit masks
+// (Props/ASM_Prop.py:245-306).  conj for the adjoint.
+__device__ __forceinline__ float2 tf_value(const AsmArgs& a, const TfScalars& s, float Kx, float Ky) {
+  const float Kx2 = Kx * Kx, Ky2 = Ky * Ky;
+  const float K2 = Kx2 + Ky2;
+  const float d = s.kl2 - K2;
+  if (d < 0.0f) return make_float2(0.f, 0.f);
+  if (a.bl == THZ_BANDLIMIT_EXACT) {
+    const bool c1 = (Kx2 / s.A + Ky2 / s.kl2) <= 1.0f;
+    const bool c2 = (Kx2 / s.kl2 + Ky2 / s.Bv) <= 1.0f;
+    if (!(c1 && c2)) return make_float2(0.f, 0.f);
+  } else if (a.bl == THZ_BANDLIMIT_APPROX) {
+    if (fabsf(Kx) > s.kxm || fabsf(Ky) > s.kym) return make_float2(0.f, 0.f);
+  }
+  const float ang = s.z * sqrtf(d);
+  float sn, cs;
+  sincos_rad(ang, &sn, &cs);
+  return make_float2(cs, a.adjoint ? -sn : sn);
+}
+#pragma clang fp contract(on)
+
+// ---------------------------------------------------------------------------------------------
+// K1: row FFT of the zero-padded input rows -> band columns, column-major T[bc][c][h]
+// ---------------------------------------------------------------------------------------------
+// PN > 0: compile-time power-of-two transform (blockDim == PN / FFT_MAXV); PN == 0: runtime plan.
+template <int PN, bool INV>
+__device__ __forceinline__ void run_fft(float2* lds, const FftPlan& p, int tid, int nt) {
+  if constexpr (PN > 0) fft_pow2<INV, PN, PN / FFT_MAXV>(lds, p.tw, tid);
+  else fft_lds<INV>(lds, p, tid, nt);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
+                                                    FftPlan pw, AsmArgs a) {
+  extern __shared__ float2 lds[];
+  const int row = xcd_rows(blockIdx.x, gridDim.x);
+  const int bc = row / a.Hin, h = row - bc * a.Hin;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float2* src = in + ((size_t)bc * a.Hin + h) * a.Win;
+  for (int j = tid; j < a.Pw; j += nt) {
+    const int s = j - a.in_c0;
+    lds[padx(j)] = (s >= 0 && s < a.Win) ? src[s] : make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  run_fft<PN, false>(lds, pw, tid, nt);
+  float2* dst = T + (size_t)bc * a.ncols * a.Hin + h;
+  for (int c = tid; c < a.ncols; c += nt) {
+    int j = c - a.J;
+    if (j < 0) j += a.Pw;
+    dst[(size_t)c * a.Hin] = lds[padx(j)];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
+// ---------------------------------------------------------------------------------------------
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                AsmArgs a) {
+  extern __shared__ float2 lds[];
+  const int c = blockIdx.x, bc = blockIdx.y;
+  const int nt = blockDim.x;
+  const int Ph = a.Ph;
+  // Each phase works from its own opaque copy of threadIdx.x: otherwise the compiler CSEs /
+  // hoists the forward and inverse transforms' LDS addresses and twiddle loads across the
+  // whole kernel and spills (the two transforms share every twiddle address).
+  int tid = threadIdx.x;
+  const float2* col = T + ((size_t)bc * a.ncols + c) * a.Hin;
+  for (int i = tid; i < Ph; i += nt) {
+    const int s = i - a.in_r0;
+    lds[padx(i)] = (s >= 0 && s < a.Hin) ? col[s] : make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  run_fft<PN, false>(lds, ph, tid, nt);
+  float2 sp[FFT_MAXV];
+  asm volatile("" : "+v"(tid));
+#pragma unroll
+  for (int m = 0; m < FFT_MAXV; ++m) {
+    const int i = tid + m * nt;
+    sp[m] = i < Ph ? lds[padx(i)] : make_float2(0.f, 0.f);
+  }
+  const float lam = a.lam[bc % a.C];
+  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
+  for (int zz = 0; zz < a.nz; ++zz) {
+    const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+    int tm = threadIdx.x;
+    asm volatile("" : "+v"(tm));
+    __syncthreads();  // previous z's readers are done with lds
+#pragma unroll
+    for (int m = 0; m < FFT_MAXV; ++m) {
+      const int i = tm + m * nt;
+      if (i < Ph) {
+        const float2 hv = tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky);
+        lds[padx(i)] = cmul(sp[m], hv);
+      }
+    }
+    __syncthreads();
+    int tz = threadIdx.x;
+    asm volatile("" : "+v"(tz));
+    run_fft<PN, true>(lds, ph, tz, nt);
+    float2* dst = U + (((size_t)zz * a.BC + bc) * a.ncols + c) * a.Hout;
+    for (int r = tz; r < a.Hout; r += nt) dst[r] = cscale(lds[padx(a.out_r0 + r)], a.scale);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3: per output row: gather band from U, IFFT(Pw), crop -> out[z][bc][r][w]
+// ---------------------------------------------------------------------------------------------
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ U, float2* __restrict__ out,
+                                                    FftPlan pw, AsmArgs a) {
+  extern __shared__ float2 lds[];
+  const int row = xcd_rows(blockIdx.x, gridDim.x);  // row in [0, nz*BC*Hout)
+  const int plane = row / a.Hout, r = row - plane * a.Hout;  // plane = zz*BC + bc
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const float2* src = U + (size_t)plane * a.ncols * a.Hout + r;
+  for (int j = tid; j < a.Pw; j += nt) {
+    const int c = freq_index(j, a.Pw) + a.J;
+    lds[padx(j)] = (c >= 0 && c < a.ncols) ? src[(size_t)c * a.Hout] : make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  run_fft<PN, true>(lds, pw, tid, nt);
+  float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
+  for (int w = tid; w < a.Wout; w += nt) dst[w] = lds[padx(a.out_c0 + w)];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Generic batched row FFT (building block / diagnostics)
+// ---------------------------------------------------------------------------------------------
+template <int PN>
+__global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict__ in, float2* __restrict__ out,
+                                                       FftPlan p, int inverse) {
+  extern __shared__ float2 lds[];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const size_t base = (size_t)blockIdx.x * p.n;
+  for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];
+  __syncthreads();
+  if (inverse) run_fft<PN, true>(lds, p, tid, nt);
+  else run_fft<PN, false>(lds, p, tid, nt);
+  for (int j = tid; j < p.n; j += nt) out[base + j] = lds[padx(j)];
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------------
+struct AsmGeom {
+  int BC, Ph, Pw, ncols, J, Hin, Win, Hout, Wout, zc;
+};
+
+static int validate(const thz_asm_desc* d) {
+  if (!d) return fail(THZ_E_ARG, "null descriptor");
+  if (d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1 || d->pad_h < 0 || d->pad_w < 0)
+    return fail(THZ_E_ARG, "bad shape B=%d C=%d H=%d W=%d pad=(%d,%d)", d->B, d->C, d->H, d->W, d->pad_h, d->pad_w);
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d wavelengths", d->C, THZ_MAX_WAVELENGTHS);
+  if (d->Z < 1 || d->Z > THZ_MAX_Z) return fail(THZ_E_UNSUPPORTED, "Z=%d outside [1, %d]", d->Z, THZ_MAX_Z);
+  if (d->adjoint && d->Z != 1) return fail(THZ_E_ARG, "adjoint needs Z == 1 (got %d)", d->Z);
+  if (d->bandlimit < 0 || d->bandlimit > 2) return fail(THZ_E_ARG, "bad bandlimit %d", d->bandlimit);
+  if (!d->wavelengths || !d->z) return fail(THZ_E_ARG, "null wavelengths / z");
+  if (!(d->dx > 0.f) || !(d->dy > 0.f)) return fail(THZ_E_ARG, "spacing must be > 0");
+  const int Ph = d->H + 2 * d->pad_h, Pw = d->W + 2 * d->pad_w;
+  if (Ph > FFT_MAX_N || Pw > FFT_MAX_N)
+    return fail(THZ_E_UNSUPPORTED, "padded size %dx%d exceeds %d", Ph, Pw, FFT_MAX_N);
+  for (int c = 0; c < d->C; ++c)
+    if (!(d->wavelengths[c] > 0.f)) return fail(THZ_E_ARG, "wavelength[%d] must be > 0", c);
+  return THZ_OK;
+}
+
+// Largest |m_y| with a possibly non-zero H over all (wavelength, z); +2 columns margin for
+// the fp32-vs-double evaluation.  Exact: Ky^2 <= min(k^2, (2 pi v_lim)^2); approx: |Ky| <=
+// min(k, k_y_max); none: evanescent only.  All maxima sit on the Kx = 0 row.
+static int band_half_width(const thz_asm_desc* d, int Ph, int Pw) {
+  double kymax = 0.0;
+  const double dy = d->dy, dx = d->dx;
+  for (int c = 0; c < d->C; ++c) {
+    const double lam = d->wavelengths[c];
+    const double kl = 2.0 * M_PI / lam;
+    for (int zi = 0; zi < d->Z; ++zi) {
+      const double z = d->z[zi];
+      double lim = kl;
+      if (d->bandlimit == THZ_BANDLIMIT_EXACT) {
+        const double dv = 1.0 / (2.0 * Ph * dy);
+        const double vl = 1.0 / std::sqrt(std::pow(2.0 * dv * z, 2) + 1.0) / lam;
+        lim = std::min(lim, 2.0 * M_PI * vl);
+      } else if (d->bandlimit == THZ_BANDLIMIT_APPROX) {
+        const double ly = Ph * dy;
+        const double kym = 2.0 * M_PI / std::sqrt(std::pow(2.0 * z / ly, 2) + 1.0) / lam;
+        lim = std::min(lim, kym);
+      }
+      kymax = std::max(kymax, lim);
+    }
+  }
+  (void)dx;
+  const double dky = 2.0 * M_PI / (Pw * dy);
+  const double j = std::floor(kymax / dky) + 2.0;
+  if (j >= Pw / 2) return -1;  // full band
+  return (int)j;
+}
+
+static void geometry(const thz_asm_desc* d, AsmGeom* g) {
+  g->BC = d->B * d->C;
+  g->Ph = d->H + 2 * d->pad_h;
+  g->Pw = d->W + 2 * d->pad_w;
+  const int Ho = d->unpad ? d->H : g->Ph, Wo = d->unpad ? d->W : g->Pw;
+  if (!d->adjoint) {
+    g->Hin = d->H; g->Win = d->W; g->Hout = Ho; g->Wout = Wo;
+  } else {
+    g->Hin = Ho; g->Win = Wo; g->Hout = d->H; g->Wout = d->W;
+  }
+  const int J = band_half_width(d, g->Ph, g->Pw);
+  if (J < 0) {
+    g->ncols = g->Pw;
+    g->J = g->Pw / 2;
+  } else {
+    g->ncols = 2 * J + 1;
+    g->J = J;
+  }
+  int zc = d->z_chunk > 0 ? d->z_chunk : 0;
+  if (zc == 0) {
+    // default: keep the per-chunk U intermediate around 128 MiB (Infinity-Cache sized)
+    const double per_z = (double)g->BC * g->ncols * g->Hout * sizeof(float2);
+    zc = (int)std::max(1.0, std::floor((128.0 * 1024 * 1024) / per_z));
+  }
+  g->zc = std::min(zc, d->adjoint ? 1 : d->Z);
+}
+
+// Compile-time power-of-two instantiations (blockDim = n / FFT_MAXV); 0 = runtime plan.
+static int pow2_kind(int n) {
+  switch (n) {
+    case 1024: case 2048: case 4096: case 8192: case 16384: return n;
+    default: return 0;
+  }
+}
+static int threads_for(int n) { return pow2_kind(n) ? n / FFT_MAXV : fft_threads(n); }
+
+#define THZ_POW2_SWITCH(n, KER, ...)                                                              \
+  switch (pow2_kind(n)) {                                                                          \
+    case 1024: hipLaunchKernelGGL(KER<1024>, __VA_ARGS__); break;                                  \
+    case 2048: hipLaunchKernelGGL(KER<2048>, __VA_ARGS__); break;                                  \
+    case 4096: hipLaunchKernelGGL(KER<4096>, __VA_ARGS__); break;                                  \
+    case 8192: hipLaunchKernelGGL(KER<8192>, __VA_ARGS__); break;                                  \
+    case 16384: hipLaunchKernelGGL(KER<16384>, __VA_ARGS__); break;                                \
+    default: hipLaunchKernelGGL(KER<0>, __VA_ARGS__); break;                                       \
+  }
+
+template <int PN>
+static void add_kernels(std::vector<const void*>& ks) {
+  ks.push_back((const void*)asm_rows_fwd<PN>);
+  ks.push_back((const void*)asm_cols<PN>);
+  ks.push_back((const void*)asm_rows_inv<PN>);
+  ks.push_back((const void*)fft_rows_kernel<PN>);
+}
+
+// Workgroups above 64 KiB of dynamic LDS must opt in once per kernel.
+static int ensure_lds_attr() {
+  static std::once_flag once;
+  static hipError_t err = hipSuccess;
+  std::call_once(once, [] {
+    const int mx = (int)fft_lds_bytes(FFT_MAX_N);
+    std::vector<const void*> ks;
+    add_kernels<0>(ks);
+    add_kernels<1024>(ks);
+    add_kernels<2048>(ks);
+    add_kernels<4096>(ks);
+    add_kernels<8192>(ks);
+    add_kernels<16384>(ks);
+    for (const void* k : ks) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      if (e != hipSuccess) err = e;
+    }
+  });
+  if (err != hipSuccess) return fail(THZ_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s",
+                                     hipGetErrorString(err));
+  return THZ_OK;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static size_t ws_bytes(const AsmGeom& g) {
+  return align256((size_t)g.BC * g.ncols * g.Hin * sizeof(float2)) +
+         align256((size_t)g.zc * g.BC * g.ncols * g.Hout * sizeof(float2));
+}
+
+}  // namespace thz
+
+using namespace thz;
+
+extern "C" int thz_asm_band(const thz_asm_desc* d, int* ncols) {
+  int e = validate(d);
+  if (e) return e;
+  AsmGeom g;
+  geometry(d, &g);
+  if (ncols) *ncols = g.ncols;
+  return THZ_OK;
+}
+
+extern "C" int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes) {
+  int e = validate(d);
+  if (e) return e;
+  if (!bytes) return fail(THZ_E_ARG, "null bytes");
+  AsmGeom g;
+  geometry(d, &g);
+  *bytes = ws_bytes(g);
+  return THZ_OK;
+}
+
+extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* workspace,
+                               size_t workspace_bytes, thz_stream_t stream) {
+  int e = validate(d);
+  if (e) return e;
+  if (!in || !out) return fail(THZ_E_ARG, "null data pointer");
+  AsmGeom g;
+  geometry(d, &g);
+  const size_t need = ws_bytes(g);
+  if (!workspace || workspace_bytes < need)
+    return fail(THZ_E_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+  FftPlan pw, ph;
+  if ((e = get_plan(g.Pw, &pw))) return e;
+  if ((e = get_plan(g.Ph, &ph))) return e;
+
+  AsmArgs a{};
+  a.BC = g.BC;
+  a.C = d->C;
+  a.Ph = g.Ph;
+  a.Pw = g.Pw;
+  const int Ho = d->unpad ? d->H : g.Ph, Wo = d->unpad ? d->W : g.Pw;
+  const int o_r0 = d->unpad ? d->pad_h : 0, o_c0 = d->unpad ? d->pad_w : 0;
+  if (!d->adjoint) {
+    a.in_r0 = d->pad_h; a.in_c0 = d->pad_w; a.Hin = d->H; a.Win = d->W;
+    a.out_r0 = o_r0; a.out_c0 = o_c0; a.Hout = Ho; a.Wout = Wo;
+  } else {
+    a.in_r0 = o_r0; a.in_c0 = o_c0; a.Hin = Ho; a.Win = Wo;
+    a.out_r0 = d->pad_h; a.out_c0 = d->pad_w; a.Hout = d->H; a.Wout = d->W;
+  }
+  a.ncols = g.ncols;
+  a.J = g.J;
+  a.bl = d->bandlimit;
+  a.adjoint = d->adjoint;
+  a.dx = d->dx;
+  a.dy = d->dy;
+  a.scale = (float)(1.0 / ((double)g.Ph * (double)g.Pw));
+  for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
+  for (int zi = 0; zi < d->Z; ++zi) a.zv[zi] = d->z[zi];
+
+  hipStream_t s = (hipStream_t)stream;
+  if ((e = ensure_lds_attr())) return e;
+  float2* T = (float2*)workspace;
+  float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncols * g.Hin * sizeof(float2)));
+  const int tw = threads_for(g.Pw), th = threads_for(g.Ph);
+
+  {
+    KernelTimer kt("asm_rows_fwd", s);
+    THZ_POW2_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), dim3(tw), fft_lds_bytes(g.Pw), s, (const float2*)in,
+                    T, pw, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  for (int z0 = 0; z0 < d->Z; z0 += g.zc) {
+    a.zoff = z0;
+    a.nz = std::min(g.zc, d->Z - z0);
+    {
+      KernelTimer kt("asm_cols", s);
+      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols, g.BC), dim3(th), fft_lds_bytes(g.Ph), s, (const float2*)T, U,
+                      ph, a);
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+    {
+      KernelTimer kt("asm_rows_inv", s);
+      THZ_POW2_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), dim3(tw), fft_lds_bytes(g.Pw), s,
+                      (const float2*)U, (float2*)out, pw, a);
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+  }
+  return THZ_OK;
+}
+
+extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream) {
+  if (!in || !out || rows < 1) return fail(THZ_E_ARG, "bad fft_rows arguments");
+  FftPlan p;
+  int e = get_plan(n, &p);
+  if (e) return e;
+  if ((e = ensure_lds_attr())) return e;
+  THZ_POW2_SWITCH(n, fft_rows_kernel, dim3(rows), dim3(threads_for(n)), fft_lds_bytes(n), (hipStream_t)stream,
+                  (const float2*)in, (float2*)out, p, inverse);
+  THZ_LAUNCH_CHECK();
+  return THZ_OK;
+}

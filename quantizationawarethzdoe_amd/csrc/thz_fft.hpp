@@ -1,0 +1,359 @@
+// LDS-resident mixed-radix Stockham FFT engine for gfx950 (CDNA4, wave64).
+//
+// One workgroup transforms one (or several) length-N complex rows held in LDS in
+// natural order.  Radices 2/4/8/16 (and 3/5/7) run as in-register butterflies; any
+// other factor (large primes such as 67, 101, 251 that the reference's
+// P = N + 2*floor(s*N/2) padding produces) runs through a generic DFT stage that
+// reads the twiddle table directly, so every length is supported.
+//
+// Stockham autosort, stage with current sub-transform length L and radix R:
+//   butterfly i in [0, N/R), k = i mod L:
+//     v_r = x[i + r*N/R] * w^(r*k),  w = exp(-+2 pi i /(L R))
+//     y[(i-k)*R + k + q*L] = DFT_R(v)_q
+// The twiddle table holds exp(-2 pi i t / N), t in [0, N), computed in double on
+// the host (thz_plan.cpp) and read through L1/L2 (a few KiB, always cache-resident).
+//
+// LDS addressing pads one float2 every 16 (PADX) so power-of-two strides spread
+// over the 64 LDS banks.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace thz {
+
+constexpr int FFT_MAX_STAGES = 24;
+constexpr int FFT_MAXV = 16;  // complex values held per thread per stage (N <= 16 * threads)
+
+struct FftPlan {
+  int n;                       // transform length
+  int nst;                     // number of stages
+  int radix[FFT_MAX_STAGES];   // radix of each stage (product == n)
+  const float2* tw;            // n roots exp(-2 pi i t / n)
+};
+
+__device__ __forceinline__ int padx(int a) { return a + (a >> 4); }
+__host__ __device__ constexpr int lds_floats2(int n) { return n + (n >> 4) + 1; }
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// multiply by -i (forward) or +i (inverse)
+template <bool INV>
+__device__ __forceinline__ float2 mul_mi(float2 a) {
+  return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
+}
+
+// ---------------------------------------------------------------------------------------------
+// In-register DFTs: y_q = sum_r v_r exp(-+2 pi i r q / R)
+// ---------------------------------------------------------------------------------------------
+template <bool INV>
+__device__ __forceinline__ void dft2(float2& a, float2& b) {
+  float2 t = a;
+  a = cadd(t, b);
+  b = csub(t, b);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
+  float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
+  float2 t2 = cadd(a1, a3), t3 = mul_mi<INV>(csub(a1, a3));
+  a0 = cadd(t0, t2);
+  a2 = csub(t0, t2);
+  a1 = cadd(t1, t3);
+  a3 = csub(t1, t3);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft8(float2* v) {
+  // even/odd split: E = DFT4(v0,v2,v4,v6), O = DFT4(v1,v3,v5,v7)
+  float2 e0 = v[0], e1 = v[2], e2 = v[4], e3 = v[6];
+  float2 o0 = v[1], o1 = v[3], o2 = v[5], o3 = v[7];
+  dft4<INV>(e0, e1, e2, e3);
+  dft4<INV>(o0, o1, o2, o3);
+  const float c = 0.70710678118654752440f;
+  // w8^1 * o1, w8^2 * o2, w8^3 * o3 ; w8 = exp(-+i pi/4)
+  float2 t1, t2, t3;
+  if (!INV) {
+    t1 = make_float2(c * (o1.x + o1.y), c * (o1.y - o1.x));
+    t2 = make_float2(o2.y, -o2.x);
+    t3 = make_float2(c * (o3.y - o3.x), -c * (o3.x + o3.y));
+  } else {
+    t1 = make_float2(c * (o1.x - o1.y), c * (o1.y + o1.x));
+    t2 = make_float2(-o2.y, o2.x);
+    t3 = make_float2(-c * (o3.x + o3.y), c * (o3.x - o3.y));
+  }
+  v[0] = cadd(e0, o0);
+  v[4] = csub(e0, o0);
+  v[1] = cadd(e1, t1);
+  v[5] = csub(e1, t1);
+  v[2] = cadd(e2, t2);
+  v[6] = csub(e2, t2);
+  v[3] = cadd(e3, t3);
+  v[7] = csub(e3, t3);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft16(float2* v) {
+  // 16 = 4 x 4: B[r2][q1] = DFT4_{r1}(v[r2 + 4 r1]); B *= w16^(r2 q1); y[q1 + 4 q2] = DFT4_{r2}(B[.][q1])
+  float2 b[4][4];
+#pragma unroll
+  for (int r2 = 0; r2 < 4; ++r2) {
+    b[r2][0] = v[r2];
+    b[r2][1] = v[r2 + 4];
+    b[r2][2] = v[r2 + 8];
+    b[r2][3] = v[r2 + 12];
+    dft4<INV>(b[r2][0], b[r2][1], b[r2][2], b[r2][3]);
+  }
+  const float s = INV ? 1.f : -1.f;
+  // w16^k = cos(2 pi k/16) + s i sin(2 pi k/16), k = r2*q1 in {1,2,3,4,6,9}
+  const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
+  const float c2 = 0.70710678118654752440f;
+  b[1][1] = cmul(b[1][1], make_float2(c1, s * s1));
+  b[1][2] = cmul(b[1][2], make_float2(c2, s * c2));
+  b[1][3] = cmul(b[1][3], make_float2(s1, s * c1));
+  b[2][1] = cmul(b[2][1], make_float2(c2, s * c2));
+  b[2][2] = mul_mi<INV>(b[2][2]);
+  b[2][3] = cmul(b[2][3], make_float2(-c2, s * c2));
+  b[3][1] = cmul(b[3][1], make_float2(s1, s * c1));
+  b[3][2] = cmul(b[3][2], make_float2(-c2, s * c2));
+  b[3][3] = cmul(b[3][3], make_float2(-c1, -s * s1));
+#pragma unroll
+  for (int q1 = 0; q1 < 4; ++q1) {
+    float2 a0 = b[0][q1], a1 = b[1][q1], a2 = b[2][q1], a3 = b[3][q1];
+    dft4<INV>(a0, a1, a2, a3);
+    v[q1] = a0;
+    v[q1 + 4] = a1;
+    v[q1 + 8] = a2;
+    v[q1 + 12] = a3;
+  }
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft3(float2* v) {
+  const float c = -0.5f, s = (INV ? 1.f : -1.f) * 0.86602540378443864676f;
+  float2 t = cadd(v[1], v[2]);
+  float2 d = csub(v[1], v[2]);
+  float2 m = make_float2(v[0].x + c * t.x, v[0].y + c * t.y);
+  float2 js = make_float2(-s * d.y, s * d.x);  // i*s*d
+  v[0] = cadd(v[0], t);
+  v[1] = cadd(m, js);
+  v[2] = csub(m, js);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft5(float2* v) {
+  const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+  const float sg = INV ? 1.f : -1.f;
+  const float s1 = sg * 0.95105651629515357212f, s2 = sg * 0.58778525229247312917f;
+  float2 a = cadd(v[1], v[4]), b = csub(v[1], v[4]);
+  float2 c = cadd(v[2], v[3]), d = csub(v[2], v[3]);
+  float2 x0 = v[0];
+  float2 m1 = make_float2(x0.x + c1 * a.x + c2 * c.x, x0.y + c1 * a.y + c2 * c.y);
+  float2 m2 = make_float2(x0.x + c2 * a.x + c1 * c.x, x0.y + c2 * a.y + c1 * c.y);
+  // n1 = i*(s1 b + s2 d), n2 = i*(s2 b - s1 d)
+  float2 p1 = make_float2(s1 * b.x + s2 * d.x, s1 * b.y + s2 * d.y);
+  float2 p2 = make_float2(s2 * b.x - s1 * d.x, s2 * b.y - s1 * d.y);
+  float2 n1 = make_float2(-p1.y, p1.x), n2 = make_float2(-p2.y, p2.x);
+  v[0] = make_float2(x0.x + a.x + c.x, x0.y + a.y + c.y);
+  v[1] = cadd(m1, n1);
+  v[4] = csub(m1, n1);
+  v[2] = cadd(m2, n2);
+  v[3] = csub(m2, n2);
+}
+
+template <bool INV>
+__device__ __forceinline__ void dft7(float2* v) {
+  const float sg = INV ? 1.f : -1.f;
+  const float c1 = 0.62348980185873353053f, c2 = -0.22252093395631440429f, c3 = -0.90096886790241912624f;
+  const float s1 = sg * 0.78183148246802980871f, s2 = sg * 0.97492791218182360702f,
+              s3 = sg * 0.43388373911755812048f;
+  float2 a1 = cadd(v[1], v[6]), b1 = csub(v[1], v[6]);
+  float2 a2 = cadd(v[2], v[5]), b2 = csub(v[2], v[5]);
+  float2 a3 = cadd(v[3], v[4]), b3 = csub(v[3], v[4]);
+  float2 x0 = v[0];
+  float2 m1 = make_float2(x0.x + c1 * a1.x + c2 * a2.x + c3 * a3.x, x0.y + c1 * a1.y + c2 * a2.y + c3 * a3.y);
+  float2 m2 = make_float2(x0.x + c2 * a1.x + c3 * a2.x + c1 * a3.x, x0.y + c2 * a1.y + c3 * a2.y + c1 * a3.y);
+  float2 m3 = make_float2(x0.x + c3 * a1.x + c1 * a2.x + c2 * a3.x, x0.y + c3 * a1.y + c1 * a2.y + c2 * a3.y);
+  float2 p1 = make_float2(s1 * b1.x + s2 * b2.x + s3 * b3.x, s1 * b1.y + s2 * b2.y + s3 * b3.y);
+  float2 p2 = make_float2(s2 * b1.x - s3 * b2.x - s1 * b3.x, s2 * b1.y - s3 * b2.y - s1 * b3.y);
+  float2 p3 = make_float2(s3 * b1.x - s1 * b2.x + s2 * b3.x, s3 * b1.y - s1 * b2.y + s2 * b3.y);
+  v[0] = make_float2(x0.x + a1.x + a2.x + a3.x, x0.y + a1.y + a2.y + a3.y);
+  v[1] = make_float2(m1.x - p1.y, m1.y + p1.x);
+  v[6] = make_float2(m1.x + p1.y, m1.y - p1.x);
+  v[2] = make_float2(m2.x - p2.y, m2.y + p2.x);
+  v[5] = make_float2(m2.x + p2.y, m2.y - p2.x);
+  v[3] = make_float2(m3.x - p3.y, m3.y + p3.x);
+  v[4] = make_float2(m3.x + p3.y, m3.y - p3.x);
+}
+
+template <int R, bool INV>
+__device__ __forceinline__ void dftR(float2* v) {
+  if constexpr (R == 2) dft2<INV>(v[0], v[1]);
+  else if constexpr (R == 3) dft3<INV>(v);
+  else if constexpr (R == 4) dft4<INV>(v[0], v[1], v[2], v[3]);
+  else if constexpr (R == 5) dft5<INV>(v);
+  else if constexpr (R == 7) dft7<INV>(v);
+  else if constexpr (R == 8) dft8<INV>(v);
+  else if constexpr (R == 16) dft16<INV>(v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// One Stockham stage with a register butterfly, in place in LDS (read all, barrier, write all)
+// ---------------------------------------------------------------------------------------------
+template <int R, bool INV>
+__device__ __noinline__ void stage_reg(float2* lds, int n, int L, const float2* __restrict__ tw, int tid,
+                                          int nthr) {
+  constexpr int MAXB = (FFT_MAXV + R - 1) / R;
+  const int nb = n / R;
+  const int twstep = n / (L * R);
+  float2 v[MAXB][R];
+#pragma unroll
+  for (int m = 0; m < MAXB; ++m) {
+    const int i = tid + m * nthr;
+    if (i < nb) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[m][r] = lds[padx(i + r * nb)];
+      if (L > 1) {
+        const int k = i % L;
+        float2 w = tw[k * twstep];
+        if (INV) w.y = -w.y;
+        float2 wr = w;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          v[m][r] = cmul(v[m][r], wr);
+          if (r + 1 < R) wr = cmul(wr, w);
+        }
+      }
+      dftR<R, INV>(v[m]);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < MAXB; ++m) {
+    const int i = tid + m * nthr;
+    if (i < nb) {
+      const int k = i % L;
+      const int j = (i - k) * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) lds[padx(j + r * L)] = v[m][r];
+    }
+  }
+  __syncthreads();
+}
+
+// Generic-radix stage (any R): each thread computes FFT_MAXV outputs straight from the table.
+template <bool INV>
+__device__ __noinline__ void stage_generic(float2* lds, int n, int L, int R, const float2* __restrict__ tw,
+                                           int tid, int nthr) {
+  const int nb = n / R;
+  const int LR = L * R;
+  const int twstep = n / LR;
+  float2 out[FFT_MAXV];
+#pragma unroll
+  for (int m = 0; m < FFT_MAXV; ++m) {
+    const int o = tid + m * nthr;
+    out[m] = make_float2(0.f, 0.f);
+    if (o < n) {
+      const int k = o % L;
+      const int q = (o / L) % R;
+      const int b = o / LR;
+      const int i = b * L + k;
+      const int e = k + q * L;  // exponent numerator over L*R
+      float2 acc = make_float2(0.f, 0.f);
+      int t = 0;                 // (r * e) mod LR
+      for (int r = 0; r < R; ++r) {
+        float2 w = tw[t * twstep];
+        if (INV) w.y = -w.y;
+        float2 x = lds[padx(i + r * nb)];
+        acc.x += x.x * w.x - x.y * w.y;
+        acc.y += x.x * w.y + x.y * w.x;
+        t += e;
+        if (t >= LR) t -= LR;
+      }
+      out[m] = acc;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < FFT_MAXV; ++m) {
+    const int o = tid + m * nthr;
+    if (o < n) lds[padx(o)] = out[m];
+  }
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Compile-time power-of-two path: N, the thread count T = N/FFT_MAXV and every stage's L
+// and R are template constants, so index math is shifts/masks and loops fully unroll.
+// Radix-16 stages first, then one 8/4/2 stage for the remainder.
+// ---------------------------------------------------------------------------------------------
+template <int R, bool INV, int N, int L, int T>
+__device__ __forceinline__ void stage_ct(float2* lds, const float2* __restrict__ tw, int tid) {
+  constexpr int NB = N / R;
+  constexpr int MB = NB / T;  // butterflies per thread (exact)
+  static_assert(MB * T == NB, "pow2 plan must tile exactly");
+  constexpr int TWS = N / (L * R);
+  float2 v[MB][R];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int i = tid + m * T;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[m][r] = lds[padx(i + r * NB)];
+    if constexpr (L > 1) {
+      const int k = i & (L - 1);
+      float2 w = tw[k * TWS];
+      if (INV) w.y = -w.y;
+      float2 wr = w;
+#pragma unroll
+      for (int r = 1; r < R; ++r) {
+        v[m][r] = cmul(v[m][r], wr);
+        if (r + 1 < R) wr = cmul(wr, w);
+      }
+    }
+    dftR<R, INV>(v[m]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int i = tid + m * T;
+    const int k = i & (L - 1);
+    const int j = (i - k) * R + k;
+#pragma unroll
+    for (int r = 0; r < R; ++r) lds[padx(j + r * L)] = v[m][r];
+  }
+  __syncthreads();
+}
+
+template <bool INV, int N, int T, int L = 1>
+__device__ __forceinline__ void fft_pow2(float2* lds, const float2* __restrict__ tw, int tid) {
+  if constexpr (L < N) {
+    constexpr int REM = N / L;
+    constexpr int R = REM >= 16 ? 16 : REM;
+    stage_ct<R, INV, N, L, T>(lds, tw, tid);
+    fft_pow2<INV, N, T, L * R>(lds, tw, tid);
+  }
+}
+
+// Full transform of one row held in LDS (natural order in and out).  Unnormalised.
+template <bool INV>
+__device__ void fft_lds(float2* lds, const FftPlan& p, int tid, int nthr) {
+  int L = 1;
+  for (int s = 0; s < p.nst; ++s) {
+    const int R = p.radix[s];
+    switch (R) {
+      case 16: stage_reg<16, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      case 8: stage_reg<8, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      case 4: stage_reg<4, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      case 2: stage_reg<2, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      case 3: stage_reg<3, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      case 5: stage_reg<5, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      case 7: stage_reg<7, INV>(lds, p.n, L, p.tw, tid, nthr); break;
+      default: stage_generic<INV>(lds, p.n, L, R, p.tw, tid, nthr); break;
+    }
+    L *= R;
+  }
+}
+
+}  // namespace thz

@@ -1,0 +1,122 @@
+"""Device entry points for the propagators: thin torch glue over the C-ABI.
+
+Each function takes CUDA(HIP) complex64 tensors plus HOST scalars (wavelengths,
+spacing, z) and enqueues the hand-written gfx950 kernels of libthzdoe.so on the
+current torch stream.  The autograd Functions route backward through the same
+kernels (the ASM adjoint == ASM with conj(H)).  There is no CPU
+path: a CPU tensor is an error.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+
+
+def _require_device(t: torch.Tensor, what: str):
+    if not t.is_cuda:
+        raise RuntimeError(f"{what}: the MI355X path needs a ROCm device tensor (got device {t.device}); "
+                           "this framework has no CPU compute path")
+
+
+def _stream_handle():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def asm_padding(H, W, padding_scale, do_padding=True):
+    """pad = floor(s N / 2), P = N + 2 pad (Props/ASM_Prop.py:119-136)."""
+    if not do_padding:
+        return 0, 0
+    sh, sw = padding_scale
+    return int(math.floor(float(sh) * H / 2)), int(math.floor(float(sw) * W / 2))
+
+
+def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk=0):
+    wl = _lib.float_array(wavelengths)
+    zv = _lib.float_array(zs)
+    d = _lib.AsmDesc(B=B, C=C, H=H, W=W, pad_h=pad_h, pad_w=pad_w, unpad=int(bool(unpad)),
+                     bandlimit=int(bandlimit), Z=len(zs), adjoint=int(adjoint), z_chunk=int(z_chunk),
+                     dx=float(spacing[0]), dy=float(spacing[1]),
+                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
+                     z=ctypes.cast(zv, ctypes.POINTER(ctypes.c_float)))
+    d._keep = (wl, zv)
+    return d
+
+
+def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint=False, z_chunk=0,
+              out=None):
+    """Raw launch: forward data [B,C,H,W] -> [Z,B,C,Ho,Wo]; adjoint [1,B,C,Ho,Wo] -> [B,C,H,W]."""
+    _require_device(data, "ASM")
+    if data.dtype != torch.complex64:
+        raise TypeError(f"ASM kernels compute in complex64; got {data.dtype}")
+    L = _lib.lib()
+    data = data.contiguous()
+    if adjoint:
+        Z, B, C, Ho, Wo = data.shape
+        if Z != 1:
+            raise ValueError("adjoint takes a single z-plane")
+        H = Ho - (0 if unpad else 2 * pad_h)
+        W = Wo - (0 if unpad else 2 * pad_w)
+        out_shape = (B, C, H, W)
+    else:
+        B, C, H, W = data.shape
+        Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
+        out_shape = (len(zs), B, C, Ho, Wo)
+    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk)
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+    ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
+    if out is None:
+        out = torch.empty(out_shape, dtype=torch.complex64, device=data.device)
+    with torch.cuda.device(data.device):
+        _lib.check(L.thz_asm_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                     ctypes.c_size_t(ws.numel()), _stream_handle()))
+    return out
+
+
+def asm_band_columns(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs):
+    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False)
+    n = ctypes.c_int(0)
+    _lib.check(_lib.lib().thz_asm_band(ctypes.byref(d), ctypes.byref(n)))
+    return n.value
+
+
+class _AsmFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_chunk):
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit)
+        return asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, False, z_chunk)
+
+    @staticmethod
+    def backward(ctx, g):
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
+        g = g.contiguous()
+        gin = None
+        for k, z in enumerate(zs):
+            gk = asm_apply(g[k:k + 1], wavelengths, spacing, [z], pad_h, pad_w, unpad, bandlimit, True)
+            gin = gk if gin is None else gin + gk
+        return gin, None, None, None, None, None, None, None, None
+
+
+def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", z_chunk=0):
+    """Differentiable ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo] (HIP kernels)."""
+    bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
+    return _AsmFunction.apply(data, list(map(float, wavelengths)), tuple(map(float, spacing)),
+                              list(map(float, zs)), int(pad_h), int(pad_w), bool(unpad), bl, int(z_chunk))
+
+
+def fft_rows(x, inverse=False):
+    """Unnormalised batched 1-D FFT along the last axis with the LDS Stockham kernel."""
+    _require_device(x, "fft_rows")
+    x = x.contiguous().to(torch.complex64)
+    out = torch.empty_like(x)
+    n = x.shape[-1]
+    rows = x.numel() // n
+    with torch.cuda.device(x.device):
+        _lib.check(_lib.lib().thz_fft_rows(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                                           rows, n, int(inverse), _stream_handle()))
+    return out

@@ -1,0 +1,148 @@
+"""ASM parity on the GPU: HIP kernels (via the ASM_prop mirror and the C-ABI) vs the
+reference-generated golden fixtures and the pinned CPU oracle.
+
+Tolerance (complex fp32, stated in BASELINE.json north_star): rel-L2 <= 1e-4 against
+the fp64 golden (the reference's own fp32 error is 1e-5 .. 1.4e-4 on these cases,
+manifest "rel32vs64"), and <= 2x the reference's own fp32 error + 2e-5 against it.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import thz_oracle as orc
+from tests.golden_io import arrays, manifest, rel_l2, spacing, wavelengths
+
+pytestmark = pytest.mark.gpu
+M = manifest()
+C0 = 2.998e8
+
+
+def _dev():
+    return torch.device("cuda:0")
+
+
+def _prop_cls():
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    return ElectricField, ASM_prop
+
+
+def _run_case(case, x, grad=None):
+    EF, ASM = _prop_cls()
+    dev = _dev()
+    wl = [C0 / (f * 1e9) for f in case["f"]]
+    data = torch.from_numpy(x).to(dev)
+    if grad is not None:
+        data.requires_grad_(True)
+    field = EF(data, wavelengths=wl if len(wl) > 1 else wl[0], spacing=[case["dx"] * 1e-3, case["dy"] * 1e-3],
+               device=dev)
+    prop = ASM(z_distance=case["z"], do_padding=case.get("do_padding", True),
+               do_unpad_after_pad=case.get("unpad", True), padding_scale=case["s"], bandlimit_kernel=case["bl"],
+               bandlimit_type=case["t"], device=dev)
+    out = prop(field)
+    gin = None
+    if grad is not None:
+        out.data.backward(torch.from_numpy(grad).to(dev))
+        gin = data.grad.detach().cpu().numpy()
+    return out.data.detach().cpu().numpy(), gin
+
+
+@pytest.mark.parametrize("case", M["asm"], ids=[c["name"] for c in M["asm"]])
+def test_asm_forward_vs_golden(case):
+    A = arrays("asm")
+    k = case["name"]
+    out, _ = _run_case(case, A[f"{k}__in"])
+    assert out.shape == A[f"{k}__out64"].shape
+    e64 = rel_l2(out, A[f"{k}__out64"])
+    e32 = rel_l2(out, A[f"{k}__out32"])
+    assert e64 <= 1e-4, e64
+    assert e32 <= 2 * case["rel32vs64"] + 2e-5, (e32, case["rel32vs64"])
+
+
+@pytest.mark.parametrize("case", [c for c in M["asm"] if c["grad"]], ids=lambda c: c["name"])
+def test_asm_backward_vs_reference_autograd(case):
+    A = arrays("asm")
+    k = case["name"]
+    _, gin = _run_case(case, A[f"{k}__in"], grad=A[f"{k}__gout"])
+    assert rel_l2(gin, A[f"{k}__gin64"]) <= 1e-4
+
+
+def test_asm_cfg1_checksum():
+    """cfg1: 1024^2 ones-field, z=0.2 m, dx=0.5 mm, 300 GHz, s=1 (P=2048), exact."""
+    c = M["asm_cfg1"]
+    G = arrays("asm_cfg1")
+    out, _ = _run_case(c, np.ones((1, 1, 1024, 1024), np.complex64))
+    e = float(np.sum(np.abs(out.astype(np.complex128)) ** 2))
+    assert abs(e - c["energy64"]) / c["energy64"] < 2e-5
+    assert rel_l2(out[0, 0, ::32, ::32], G["cfg1__sub64"]) <= 1e-4
+    assert rel_l2(out[0, 0, 512, :], G["cfg1__row512_64"]) <= 1e-4
+
+
+def test_asm_multi_z_matches_oracle():
+    EF, ASM = _prop_cls()
+    dev = _dev()
+    rng = np.random.default_rng(3)
+    x = (rng.standard_normal((2, 2, 80, 72)) + 1j * rng.standard_normal((2, 2, 80, 72))).astype(np.complex64)
+    wl = [C0 / 250e9, C0 / 330e9]
+    zs = [0.02, 0.07, -0.03, 0.15, 0.3]
+    field = EF(torch.from_numpy(x).to(dev), wavelengths=wl, spacing=[0.5e-3, 0.6e-3], device=dev)
+    prop = ASM(z_distance=zs[0], padding_scale=1.5, bandlimit_type="approx", device=dev)
+    planes = prop.propagate_planes(field, zs).cpu().numpy()
+    assert planes.shape == (5, 2, 2, 80, 72)
+    for k, z in enumerate(zs):
+        ref = orc.asm_forward(torch.from_numpy(x).to(torch.complex128), wavelengths([250, 330], True),
+                              spacing(0.5, 0.6, True), z, 1.5, bandlimit_type="approx").numpy()
+        assert rel_l2(planes[k], ref) <= 1e-4, (k, z)
+
+
+@pytest.mark.parametrize("n", list(range(1, 65)) + [67, 100, 101, 128, 201, 243, 250, 251, 300, 303, 500, 1000,
+                                                    1024, 2048, 3000, 4096, 6144, 8192, 12288, 16384])
+def test_fft_rows_vs_numpy(n):
+    from quantizationawarethzdoe_amd.propagation import fft_rows
+    rng = np.random.default_rng(n)
+    rows = 3
+    x = (rng.standard_normal((rows, n)) + 1j * rng.standard_normal((rows, n))).astype(np.complex64)
+    xt = torch.from_numpy(x).to(_dev())
+    f = fft_rows(xt).cpu().numpy()
+    b = fft_rows(xt, inverse=True).cpu().numpy()
+    ref_f = np.fft.fft(x.astype(np.complex128), axis=-1)
+    ref_b = np.fft.ifft(x.astype(np.complex128), axis=-1) * n
+    tol = 2e-6 * max(1.0, np.log2(n))
+    assert rel_l2(f, ref_f) <= tol
+    assert rel_l2(b, ref_b) <= tol
+
+
+def test_asm_full_size_properties():
+    """cfg2 geometry (4096^2 Gaussian, P=8192, dx=0.25 mm, 300 GHz): one plane vs the fp32 oracle,
+    plus linearity and the adjoint identity <A x, y> = <x, A^H y> at full size."""
+    EF, ASM = _prop_cls()
+    dev = _dev()
+    N = 4096
+    dx = 0.25e-3
+    lam = C0 / 300e9
+    xs = (torch.arange(N, dtype=torch.float32) - N / 2) * dx
+    X, Y = torch.meshgrid(xs, xs, indexing="ij")
+    g = torch.exp(-(X ** 2 + Y ** 2) / (50e-3) ** 2).to(torch.complex64)[None, None]
+    prop = ASM(z_distance=0.05, padding_scale=1, device=dev)
+    f1 = EF(g.to(dev), wavelengths=lam, spacing=dx, device=dev)
+    o1 = prop(f1).data
+    with torch.no_grad():
+        torch.set_num_threads(max(1, torch.get_num_threads()))
+        ref = orc.asm_forward(g, torch.tensor([lam], dtype=torch.float32), torch.tensor([dx, dx]), 0.05, 1)
+    assert rel_l2(o1.cpu().numpy(), ref.numpy()) <= 1e-4
+    gen = torch.Generator(device=dev).manual_seed(0)
+    r = torch.randn(1, 1, N, N, dtype=torch.complex64, device=dev, generator=gen)
+    o2 = prop(EF(r, wavelengths=lam, spacing=dx, device=dev)).data
+    o3 = prop(EF(2.0 * g.to(dev) - 1j * r, wavelengths=lam, spacing=dx, device=dev)).data
+    lin = float((o3 - (2.0 * o1 - 1j * o2)).norm() / o3.norm())
+    assert lin <= 1e-5
+    from quantizationawarethzdoe_amd.propagation import asm_apply
+    y = torch.randn(1, 1, 1, N, N, dtype=torch.complex64, device=dev, generator=gen)
+    Ax = asm_apply(r, [lam], [dx, dx], [0.05], N // 2, N // 2, True, 1)
+    AHy = asm_apply(y, [lam], [dx, dx], [0.05], N // 2, N // 2, True, 1, adjoint=True)
+    lhs = torch.vdot(y.reshape(-1).to(torch.complex128), Ax.reshape(-1).to(torch.complex128))
+    rhs = torch.vdot(AHy.reshape(-1).to(torch.complex128), r.reshape(-1).to(torch.complex128))
+    assert abs(complex(lhs - rhs)) / abs(complex(lhs)) <= 1e-4
+    e_in = float((r.abs().double() ** 2).sum())
+    e_out = float((o2.abs().double() ** 2).sum())
+    assert e_out <= e_in * (1 + 1e-5)
