@@ -104,7 +104,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from quantizationawarethzdoe_amd import _lib
-    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_band_columns
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_plan_info
 
     x = gaussian(N_FIELD, DX, WAIST, dev)
     zs = z_planes(rank, world)
@@ -143,17 +143,9 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
 
     # algorithmic bytes per launch (SURVEY §8(d) byte model, pruned to the kept spectral band)
-    ncols = asm_band_columns(1, 1, N_FIELD, N_FIELD, pad, pad, True, 1, lam, sp, zs)
+    ncols, zc = asm_plan_info(1, 1, N_FIELD, N_FIELD, pad, pad, True, 1, lam, sp, zs, args.z_chunk)
     H = W = N_FIELD
-    nz = len(zs) if args.z_chunk == 0 else args.z_chunk
-    from quantizationawarethzdoe_amd.propagation import _asm_desc  # noqa: F401
-    bytes_rows_fwd = 8 * (H * W + ncols * H)
-    per_launch = {
-        "asm_rows_fwd": bytes_rows_fwd,
-    }
-    # chunking: the library default keeps U <= 128 MiB, i.e. z_chunk = floor(128 MiB / (ncols*H*8))
-    zc = args.z_chunk or max(1, int((128 * 1024 * 1024) // (ncols * H * 8)))
-    zc = min(zc, len(zs))
+    per_launch = {"asm_rows_fwd": 8 * (H * W + ncols * H)}
     per_launch["asm_cols"] = 8 * (ncols * H + zc * ncols * H)
     per_launch["asm_rows_inv"] = 8 * (zc * ncols * H + zc * H * W)
     stats = {}
@@ -180,7 +172,7 @@ def main():
         "config": {"workload": "cfg2: ASM_prop 4096x4096 Gaussian_beam -> 64 z-planes/GPU (20-120 mm), "
                                "300 GHz, dx 0.25 mm, padding_scale 1 (P=8192), exact band limit",
                    "planes_per_step_per_gpu": Z_PER_RANK, "N": N_FIELD, "P": 2 * N_FIELD,
-                   "band_columns": ncols, "parallelism": f"z-shard x{world}"},
+                   "band_columns": ncols, "z_chunk": zc, "parallelism": f"z-shard x{world}"},
         "hbm_gbs_algorithmic": round(total_alg * args.steps / elapsed / 1e9 * world, 1),
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in stats.items()},

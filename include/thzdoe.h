@@ -76,8 +76,9 @@ typedef struct thz_asm_desc {
 int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes);
 int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
                     thz_stream_t stream);
-/* Spectral column band the kernels keep (|m_y| <= J), for diagnostics/bench byte counts. */
-int thz_asm_band(const thz_asm_desc* d, int* ncols);
+/* Plan facts for diagnostics / bench byte counts: number of spectral columns the kernels
+ * keep (|m_y| <= J; ncols = 2J+1, or Pw when nothing is cut) and z-planes per column pass. */
+int thz_asm_band(const thz_asm_desc* d, int* ncols, int* z_chunk);
 
 /*
  * Batched 1-D FFT along the contiguous axis (the building block of ft2/ift2,

@@ -114,7 +114,8 @@ class ASM_prop(nn.Module):
             return
         lmax = np.float32(max(wavelengths_host))
         dx = np.array([dx], dtype=np.float32)
-        zc = (np.float32(Ph) * dx ** 2) * np.sqrt(np.float32(1) - (lmax / (np.float32(2) * dx)) ** 2) / lmax
+        with np.errstate(invalid="ignore"):  # lambda > 2 dx gives nan, as the reference prints
+            zc = (np.float32(Ph) * dx ** 2) * np.sqrt(np.float32(1) - (lmax / (np.float32(2) * dx)) ** 2) / lmax
         if z > zc[0]:
             print("The propagation distance is greater than critical distance {} m, the TF will be undersampled!"
                   .format(zc))

@@ -61,7 +61,7 @@ def _declare(lib):
     lib.thz_last_error.restype = ctypes.c_char_p
     lib.thz_asm_workspace_size.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_size_t)]
     lib.thz_asm_forward.argtypes = [ctypes.POINTER(AsmDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
-    lib.thz_asm_band.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_int)]
+    lib.thz_asm_band.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
     lib.thz_fft_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]
     lib.thz_timing_reset.argtypes = []

@@ -289,28 +289,54 @@ __device__ __noinline__ void stage_generic(float2* lds, int n, int L, int R, con
 // and R are template constants, so index math is shifts/masks and loops fully unroll.
 // Radix-16 stages first, then one 8/4/2 stage for the remainder.
 // ---------------------------------------------------------------------------------------------
+// Twiddles w^r, r = 1..R-1, of w = exp(-+2 pi i k / (L R)): powers of two straight from the
+// table (independent loads), the rest by at most three dependent complex products.
+template <int R, bool INV>
+__device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, int kt, float2* w) {
+  // w[r] for r = 1..R-1 ; kt = k * (N / (L R)) is the table index of w^1
+  w[1] = tw[kt];
+  if constexpr (R >= 4) w[2] = tw[2 * kt];
+  if constexpr (R >= 8) w[4] = tw[4 * kt];
+  if constexpr (R >= 16) w[8] = tw[8 * kt];
+  if (INV) {
+#pragma unroll
+    for (int p = 1; p < R; p <<= 1) w[p].y = -w[p].y;
+  }
+  if constexpr (R >= 4) w[3] = cmul(w[1], w[2]);
+  if constexpr (R >= 8) {
+    w[5] = cmul(w[1], w[4]);
+    w[6] = cmul(w[2], w[4]);
+    w[7] = cmul(w[3], w[4]);
+  }
+  if constexpr (R >= 16) {
+#pragma unroll
+    for (int r = 9; r < 16; ++r) w[r] = cmul(w[r - 8], w[8]);
+  }
+}
+
 template <int R, bool INV, int N, int L, int T>
 __device__ __forceinline__ void stage_ct(float2* lds, const float2* __restrict__ tw, int tid) {
   constexpr int NB = N / R;
   constexpr int MB = NB / T;  // butterflies per thread (exact)
   static_assert(MB * T == NB, "pow2 plan must tile exactly");
+  static_assert(NB % 16 == 0 && (L == 1 || L % 16 == 0), "constant-offset LDS addressing");
   constexpr int TWS = N / (L * R);
+  // padx(i + r*NB) = padx(i) + r*(NB + NB/16); likewise for the write side (L == 1 or L % 16 == 0),
+  // so each access is base + compile-time offset (folded into the ds_read/ds_write immediate).
+  constexpr int RSTR = NB + NB / 16;
+  constexpr int WSTR = L == 1 ? 1 : L + L / 16;
   float2 v[MB][R];
 #pragma unroll
   for (int m = 0; m < MB; ++m) {
     const int i = tid + m * T;
+    const float2* src = lds + padx(i);
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[m][r] = lds[padx(i + r * NB)];
+    for (int r = 0; r < R; ++r) v[m][r] = src[r * RSTR];
     if constexpr (L > 1) {
-      const int k = i & (L - 1);
-      float2 w = tw[k * TWS];
-      if (INV) w.y = -w.y;
-      float2 wr = w;
+      float2 w[R];
+      twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
 #pragma unroll
-      for (int r = 1; r < R; ++r) {
-        v[m][r] = cmul(v[m][r], wr);
-        if (r + 1 < R) wr = cmul(wr, w);
-      }
+      for (int r = 1; r < R; ++r) v[m][r] = cmul(v[m][r], w[r]);
     }
     dftR<R, INV>(v[m]);
   }
@@ -320,8 +346,9 @@ __device__ __forceinline__ void stage_ct(float2* lds, const float2* __restrict__
     const int i = tid + m * T;
     const int k = i & (L - 1);
     const int j = (i - k) * R + k;
+    float2* dst = lds + padx(j);
 #pragma unroll
-    for (int r = 0; r < R; ++r) lds[padx(j + r * L)] = v[m][r];
+    for (int r = 0; r < R; ++r) dst[r * WSTR] = v[m][r];
   }
   __syncthreads();
 }

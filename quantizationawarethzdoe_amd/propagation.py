@@ -78,11 +78,16 @@ def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, ad
     return out
 
 
+def asm_plan_info(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, z_chunk=0):
+    """(kept spectral columns, z-planes per column pass) of the library's plan."""
+    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False, z_chunk)
+    n, zc = ctypes.c_int(0), ctypes.c_int(0)
+    _lib.check(_lib.lib().thz_asm_band(ctypes.byref(d), ctypes.byref(n), ctypes.byref(zc)))
+    return n.value, zc.value
+
+
 def asm_band_columns(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs):
-    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False)
-    n = ctypes.c_int(0)
-    _lib.check(_lib.lib().thz_asm_band(ctypes.byref(d), ctypes.byref(n)))
-    return n.value
+    return asm_plan_info(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs)[0]
 
 
 class _AsmFunction(torch.autograd.Function):

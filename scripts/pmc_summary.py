@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile_asm.sh run into profiles/ (committed evidence).
+
+Writes, for round tag R:
+  profiles/R_kernel_stats.csv   -- rocprofv3 --kernel-trace --stats summary (copied)
+  profiles/R_pmc_summary.json   -- per-kernel averages of every PMC counter collected
+  profiles/pmc_traffic.json     -- HBM bytes per launch per kernel, read by bench.py
+
+HBM bytes = (FETCH_SIZE + WRITE_SIZE) * 1024.  MI355X_MICROARCH.md §HBM: FETCH_SIZE reads
+half the bytes of a 16-B/lane streaming read on gfx950 and other widths are uncalibrated;
+our kernels load 8 B/lane, and the calibration point (asm_cols reading the 134 MB T
+buffer once at z_chunk 1) read back as 0.9x the known bytes, so no x2 correction is
+applied -- see DESIGN.md.
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+
+def per_kernel(path):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(path)):
+        k = r["Kernel_Name"]
+        if "thz::" not in k:
+            continue
+        k = k.split("(")[0].replace("void thz::", "")
+        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in acc.items()}
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    summ = {}
+    for sub in ("fetch", "write", "sq"):
+        p = os.path.join(src, sub, "run_counter_collection.csv")
+        if os.path.exists(p):
+            for k, d in per_kernel(p).items():
+                summ.setdefault(k, {}).update(d)
+    traffic = {}
+    for k, d in summ.items():
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            b = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+            d["hbm_bytes_per_launch"] = b
+            traffic[k.split("<")[0]] = int(b)
+    with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as fh:
+        json.dump(summ, fh, indent=1)
+    with open(os.path.join(prof, "pmc_traffic.json"), "w") as fh:
+        json.dump(traffic, fh, indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()
