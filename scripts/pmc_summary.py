@@ -6,11 +6,12 @@ Writes, for round tag R:
   profiles/R_pmc_summary.json   -- per-kernel averages of every PMC counter collected
   profiles/pmc_traffic.json     -- HBM bytes per launch per kernel, read by bench.py
 
-HBM bytes = (FETCH_SIZE + WRITE_SIZE) * 1024.  MI355X_MICROARCH.md §HBM: FETCH_SIZE reads
-half the bytes of a 16-B/lane streaming read on gfx950 and other widths are uncalibrated;
-our kernels load 8 B/lane, and the calibration point (asm_cols reading the 134 MB T
-buffer once at z_chunk 1) read back as 0.9x the known bytes, so no x2 correction is
-applied -- see DESIGN.md.
+HBM bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.  MI355X_MICROARCH.md §HBM: FETCH_SIZE
+reads half the bytes of a wide streaming read on gfx950; calibrated here on our own 8-B/lane
+accesses: asm_rows_inv gathers exactly 16 x 134.6 MB of U per launch (z_chunk 16) and
+FETCH_SIZE read 1.09 GB (0.50x); asm_cols reads the 134.6 MB T once and read 76.6 MB
+(0.57x).  WRITE_SIZE matched the known 2.15 GB of contiguous stores of both kernels within
+1 %, so it is used as is ("Measurement").
 """
 import collections
 import csv
@@ -46,7 +47,7 @@ def main():
     traffic = {}
     for k, d in summ.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
-            b = (d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+            b = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
             d["hbm_bytes_per_launch"] = b
             traffic[k.split("<")[0]] = int(b)
     with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as fh:
