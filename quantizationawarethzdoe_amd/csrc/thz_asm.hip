@@ -133,16 +133,24 @@ __device__ __forceinline__ float2 tf_value(const AsmArgs& a, const TfScalars& s,
 }
 #pragma clang fp contract(on)
 
+// PN > 0: compile-time power-of-two transform with fused global I/O (blockDim == PN / FFT_MAXV):
+// the first Stockham stage reads its operands straight from global memory and the last
+// stage writes its results straight to global memory (coalesced in both cases), so a
+// transform costs NST-1 LDS round trips instead of NST+1.  PN == 0: runtime mixed-radix
+// plan, data staged through LDS.
+template <int PN>
+struct Geo {
+  static constexpr int T = PN > 0 ? PN / FFT_MAXV : 0;
+};
+
+__device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
+  const int c = freq_index(j, P) + J;
+  return (c >= 0 && c < ncols) ? c : -1;
+}
+
 // ---------------------------------------------------------------------------------------------
 // K1: row FFT of the zero-padded input rows -> band columns, column-major T[bc][c][h]
 // ---------------------------------------------------------------------------------------------
-// PN > 0: compile-time power-of-two transform (blockDim == PN / FFT_MAXV); PN == 0: runtime plan.
-template <int PN, bool INV>
-__device__ __forceinline__ void run_fft(float2* lds, const FftPlan& p, int tid, int nt) {
-  if constexpr (PN > 0) fft_pow2<INV, PN, PN / FFT_MAXV>(lds, p.tw, tid);
-  else fft_lds<INV>(lds, p, tid, nt);
-}
-
 template <int PN>
 __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
                                                     FftPlan pw, AsmArgs a) {
@@ -151,17 +159,29 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
   const int bc = row / a.Hin, h = row - bc * a.Hin;
   const int tid = threadIdx.x, nt = blockDim.x;
   const float2* src = in + ((size_t)bc * a.Hin + h) * a.Win;
-  for (int j = tid; j < a.Pw; j += nt) {
-    const int s = j - a.in_c0;
-    lds[padx(j)] = (s >= 0 && s < a.Win) ? src[s] : make_float2(0.f, 0.f);
-  }
-  __syncthreads();
-  run_fft<PN, false>(lds, pw, tid, nt);
   float2* dst = T + (size_t)bc * a.ncols * a.Hin + h;
-  for (int c = tid; c < a.ncols; c += nt) {
-    int j = c - a.J;
-    if (j < 0) j += a.Pw;
-    dst[(size_t)c * a.Hin] = lds[padx(j)];
+  if constexpr (PN > 0) {
+    auto ld = [&](int, int, int idx) {
+      const int s = idx - a.in_c0;
+      return (s >= 0 && s < a.Win) ? src[s] : make_float2(0.f, 0.f);
+    };
+    auto sv = [&](int, int, int j, float2 v) {
+      const int c = band_col(j, PN, a.J, a.ncols);
+      if (c >= 0) dst[(size_t)c * a.Hin] = v;
+    };
+    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
+  } else {
+    for (int j = tid; j < a.Pw; j += nt) {
+      const int s = j - a.in_c0;
+      lds[padx(j)] = (s >= 0 && s < a.Win) ? src[s] : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    fft_lds<false>(lds, pw, tid, nt);
+    for (int c = tid; c < a.ncols; c += nt) {
+      int j = c - a.J;
+      if (j < 0) j += a.Pw;
+      dst[(size_t)c * a.Hin] = lds[padx(j)];
+    }
   }
 }
 
@@ -175,45 +195,70 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
   const int c = blockIdx.x, bc = blockIdx.y;
   const int nt = blockDim.x;
   const int Ph = a.Ph;
+  const float2* col = T + ((size_t)bc * a.ncols + c) * a.Hin;
+  const float lam = a.lam[bc % a.C];
+  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
   // Each phase works from its own opaque copy of threadIdx.x: otherwise the compiler CSEs /
   // hoists the forward and inverse transforms' LDS addresses and twiddle loads across the
   // whole kernel and spills (the two transforms share every twiddle address).
   int tid = threadIdx.x;
-  const float2* col = T + ((size_t)bc * a.ncols + c) * a.Hin;
-  for (int i = tid; i < Ph; i += nt) {
-    const int s = i - a.in_r0;
-    lds[padx(i)] = (s >= 0 && s < a.Hin) ? col[s] : make_float2(0.f, 0.f);
-  }
-  __syncthreads();
-  run_fft<PN, false>(lds, ph, tid, nt);
-  float2 sp[FFT_MAXV];
-  asm volatile("" : "+v"(tid));
-#pragma unroll
-  for (int m = 0; m < FFT_MAXV; ++m) {
-    const int i = tid + m * nt;
-    sp[m] = i < Ph ? lds[padx(i)] : make_float2(0.f, 0.f);
-  }
-  const float lam = a.lam[bc % a.C];
-  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
-  for (int zz = 0; zz < a.nz; ++zz) {
-    const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
-    int tm = threadIdx.x;
-    asm volatile("" : "+v"(tm));
-    __syncthreads();  // previous z's readers are done with lds
-#pragma unroll
-    for (int m = 0; m < FFT_MAXV; ++m) {
-      const int i = tm + m * nt;
-      if (i < Ph) {
-        const float2 hv = tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky);
-        lds[padx(i)] = cmul(sp[m], hv);
-      }
+  if constexpr (PN > 0) {
+    using S = Pow2Sched<PN>;
+    constexpr int TT = Geo<PN>::T;
+    constexpr int RL = S::radix(S::NST - 1, false);  // radix of the forward's last stage
+    constexpr int MBL = PN / RL / TT;                // its butterflies per thread
+    float2 sp[MBL][RL];                              // spectrum, element i + r*PN/RL
+    auto ld0 = [&](int, int, int idx) {
+      const int s = idx - a.in_r0;
+      return (s >= 0 && s < a.Hin) ? col[s] : make_float2(0.f, 0.f);
+    };
+    auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, ph.tw, tid, ld0, sv0);
+    for (int zz = 0; zz < a.nz; ++zz) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      int tz = threadIdx.x;
+      asm volatile("" : "+v"(tz));
+      // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
+      // holds in sp: multiply by H_z on the fly in the loader
+      auto ld1 = [&](int m, int r, int idx) {
+        return cmul(sp[m][r], tf_value(a, s, kfreq(freq_index(idx, PN), PN, a.dx), Ky));
+      };
+      float2* dst = U + (((size_t)zz * a.BC + bc) * a.ncols + c) * a.Hout;
+      auto sv1 = [&](int, int, int j, float2 v) {
+        const int r = j - a.out_r0;
+        if (r >= 0 && r < a.Hout) dst[r] = cscale(v, a.scale);
+      };
+      fft_pow2_io<true, PN, TT, true, false, false>(lds, ph.tw, tz, ld1, sv1);
+    }
+  } else {
+    for (int i = tid; i < Ph; i += nt) {
+      const int s = i - a.in_r0;
+      lds[padx(i)] = (s >= 0 && s < a.Hin) ? col[s] : make_float2(0.f, 0.f);
     }
     __syncthreads();
-    int tz = threadIdx.x;
-    asm volatile("" : "+v"(tz));
-    run_fft<PN, true>(lds, ph, tz, nt);
-    float2* dst = U + (((size_t)zz * a.BC + bc) * a.ncols + c) * a.Hout;
-    for (int r = tz; r < a.Hout; r += nt) dst[r] = cscale(lds[padx(a.out_r0 + r)], a.scale);
+    fft_lds<false>(lds, ph, tid, nt);
+    float2 sp[FFT_MAXV];
+    asm volatile("" : "+v"(tid));
+#pragma unroll
+    for (int m = 0; m < FFT_MAXV; ++m) {
+      const int i = tid + m * nt;
+      sp[m] = i < Ph ? lds[padx(i)] : make_float2(0.f, 0.f);
+    }
+    for (int zz = 0; zz < a.nz; ++zz) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      int tm = threadIdx.x;
+      asm volatile("" : "+v"(tm));
+      __syncthreads();  // previous z's readers are done with lds
+#pragma unroll
+      for (int m = 0; m < FFT_MAXV; ++m) {
+        const int i = tm + m * nt;
+        if (i < Ph) lds[padx(i)] = cmul(sp[m], tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky));
+      }
+      __syncthreads();
+      fft_lds<true>(lds, ph, tm, nt);
+      float2* dst = U + (((size_t)zz * a.BC + bc) * a.ncols + c) * a.Hout;
+      for (int r = tm; r < a.Hout; r += nt) dst[r] = cscale(lds[padx(a.out_r0 + r)], a.scale);
+    }
   }
 }
 
@@ -228,14 +273,26 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   const int plane = row / a.Hout, r = row - plane * a.Hout;  // plane = zz*BC + bc
   const int tid = threadIdx.x, nt = blockDim.x;
   const float2* src = U + (size_t)plane * a.ncols * a.Hout + r;
-  for (int j = tid; j < a.Pw; j += nt) {
-    const int c = freq_index(j, a.Pw) + a.J;
-    lds[padx(j)] = (c >= 0 && c < a.ncols) ? src[(size_t)c * a.Hout] : make_float2(0.f, 0.f);
-  }
-  __syncthreads();
-  run_fft<PN, true>(lds, pw, tid, nt);
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
-  for (int w = tid; w < a.Wout; w += nt) dst[w] = lds[padx(a.out_c0 + w)];
+  if constexpr (PN > 0) {
+    auto ld = [&](int, int, int j) {
+      const int c = band_col(j, PN, a.J, a.ncols);
+      return c >= 0 ? src[(size_t)c * a.Hout] : make_float2(0.f, 0.f);
+    };
+    auto sv = [&](int, int, int j, float2 v) {
+      const int w = j - a.out_c0;
+      if (w >= 0 && w < a.Wout) dst[w] = v;
+    };
+    fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
+  } else {
+    for (int j = tid; j < a.Pw; j += nt) {
+      const int c = band_col(j, a.Pw, a.J, a.ncols);
+      lds[padx(j)] = c >= 0 ? src[(size_t)c * a.Hout] : make_float2(0.f, 0.f);
+    }
+    __syncthreads();
+    fft_lds<true>(lds, pw, tid, nt);
+    for (int w = tid; w < a.Wout; w += nt) dst[w] = lds[padx(a.out_c0 + w)];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -247,11 +304,18 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
   extern __shared__ float2 lds[];
   const int tid = threadIdx.x, nt = blockDim.x;
   const size_t base = (size_t)blockIdx.x * p.n;
-  for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];
-  __syncthreads();
-  if (inverse) run_fft<PN, true>(lds, p, tid, nt);
-  else run_fft<PN, false>(lds, p, tid, nt);
-  for (int j = tid; j < p.n; j += nt) out[base + j] = lds[padx(j)];
+  if constexpr (PN > 0) {
+    auto ld = [&](int, int, int j) { return in[base + j]; };
+    auto sv = [&](int, int, int j, float2 v) { out[base + j] = v; };
+    if (inverse) fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, p.tw, tid, ld, sv);
+    else fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, p.tw, tid, ld, sv);
+  } else {
+    for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];
+    __syncthreads();
+    if (inverse) fft_lds<true>(lds, p, tid, nt);
+    else fft_lds<false>(lds, p, tid, nt);
+    for (int j = tid; j < p.n; j += nt) out[base + j] = lds[padx(j)];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

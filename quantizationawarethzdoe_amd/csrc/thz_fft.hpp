@@ -314,24 +314,31 @@ __device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, in
   }
 }
 
-template <int R, bool INV, int N, int L, int T>
-__device__ __forceinline__ void stage_ct(float2* lds, const float2* __restrict__ tw, int tid) {
+// One compile-time stage with pluggable input and output.
+//   IN_LDS : read x[i + r*NB] from LDS (base padx(i) + constant offsets); else ld(m, r, idx)
+//   OUT_LDS: write y[j + r*L] to LDS (in place: barrier, write, barrier); else sv(m, r, idx, v)
+// For power-of-two N >= 256 every LDS access is base + compile-time offset:
+//   padx(i + r NB) = padx(i) + r NB + (r NB >> 4)       (NB % 16 == 0)
+//   padx(j + r L)  = padx(j) + r L  + (r L >> 4)        (L | 16 or 16 | L, L R >= 16 or L == 1)
+template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, class Ld, class Sv>
+__device__ __forceinline__ void stage_x(float2* lds, const float2* __restrict__ tw, int tid, Ld& ld, Sv& sv) {
   constexpr int NB = N / R;
   constexpr int MB = NB / T;  // butterflies per thread (exact)
   static_assert(MB * T == NB, "pow2 plan must tile exactly");
-  static_assert(NB % 16 == 0 && (L == 1 || L % 16 == 0), "constant-offset LDS addressing");
+  static_assert(NB % 16 == 0, "constant-offset LDS addressing");
   constexpr int TWS = N / (L * R);
-  // padx(i + r*NB) = padx(i) + r*(NB + NB/16); likewise for the write side (L == 1 or L % 16 == 0),
-  // so each access is base + compile-time offset (folded into the ds_read/ds_write immediate).
-  constexpr int RSTR = NB + NB / 16;
-  constexpr int WSTR = L == 1 ? 1 : L + L / 16;
   float2 v[MB][R];
 #pragma unroll
   for (int m = 0; m < MB; ++m) {
     const int i = tid + m * T;
-    const float2* src = lds + padx(i);
+    if constexpr (IN_LDS) {
+      const float2* src = lds + padx(i);
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[m][r] = src[r * RSTR];
+      for (int r = 0; r < R; ++r) v[m][r] = src[r * NB + ((r * NB) >> 4)];
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) v[m][r] = ld(m, r, i + r * NB);
+    }
     if constexpr (L > 1) {
       float2 w[R];
       twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
@@ -340,27 +347,74 @@ __device__ __forceinline__ void stage_ct(float2* lds, const float2* __restrict__
     }
     dftR<R, INV>(v[m]);
   }
-  __syncthreads();
+  if constexpr (OUT_LDS) {
+    __syncthreads();
 #pragma unroll
-  for (int m = 0; m < MB; ++m) {
-    const int i = tid + m * T;
-    const int k = i & (L - 1);
-    const int j = (i - k) * R + k;
-    float2* dst = lds + padx(j);
+    for (int m = 0; m < MB; ++m) {
+      const int i = tid + m * T;
+      const int k = i & (L - 1);
+      float2* dst = lds + padx((i - k) * R + k);
 #pragma unroll
-    for (int r = 0; r < R; ++r) dst[r * WSTR] = v[m][r];
+      for (int r = 0; r < R; ++r) dst[r * L + ((r * L) >> 4)] = v[m][r];
+    }
+    __syncthreads();
+  } else {
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int i = tid + m * T;
+      const int k = i & (L - 1);
+      const int j = (i - k) * R + k;
+#pragma unroll
+      for (int r = 0; r < R; ++r) sv(m, r, j + r * L, v[m][r]);
+    }
   }
-  __syncthreads();
 }
 
-template <bool INV, int N, int T, int L = 1>
-__device__ __forceinline__ void fft_pow2(float2* lds, const float2* __restrict__ tw, int tid) {
-  if constexpr (L < N) {
-    constexpr int REM = N / L;
-    constexpr int R = REM >= 16 ? 16 : REM;
-    stage_ct<R, INV, N, L, T>(lds, tw, tid);
-    fft_pow2<INV, N, T, L * R>(lds, tw, tid);
+// Radix schedule of a power-of-two N: 16s plus one remainder radix b in {2,4,8} (or none),
+// placed last (SMALL_FIRST = false) or first (true).
+template <int N>
+struct Pow2Sched {
+  static constexpr int log2n() {
+    int l = 0;
+    while ((1 << l) < N) ++l;
+    return l;
   }
+  static constexpr int LOG = log2n();
+  static constexpr int NS16 = LOG / 4;
+  static constexpr int REM = 1 << (LOG % 4);
+  static constexpr int NST = NS16 + (REM > 1 ? 1 : 0);
+  static constexpr int radix(int s, bool small_first) {
+    if (REM == 1) return 16;
+    if (small_first) return s == 0 ? REM : 16;
+    return s == NST - 1 ? REM : 16;
+  }
+};
+
+struct NoIO {
+  __device__ float2 operator()(int, int, int) const { return make_float2(0.f, 0.f); }
+  __device__ void operator()(int, int, int, float2) const {}
+};
+
+// Stages S .. NST-1 of a power-of-two transform.  Stage 0 reads through ld unless
+// FIRST_LDS; the final stage writes through sv unless LAST_LDS.
+template <bool INV, int N, int T, bool SMALL_FIRST, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1,
+          class Ld, class Sv>
+__device__ __forceinline__ void fft_pow2_io(float2* lds, const float2* __restrict__ tw, int tid, Ld& ld, Sv& sv) {
+  using P = Pow2Sched<N>;
+  if constexpr (S < P::NST) {
+    constexpr int R = P::radix(S, SMALL_FIRST);
+    constexpr bool IN_LDS = S > 0 || FIRST_LDS;
+    constexpr bool OUT_LDS = S < P::NST - 1 || LAST_LDS;
+    stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS>(lds, tw, tid, ld, sv);
+    fft_pow2_io<INV, N, T, SMALL_FIRST, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
+  }
+}
+
+// Whole transform with the data in LDS (natural order in and out).
+template <bool INV, int N, int T>
+__device__ __forceinline__ void fft_pow2(float2* lds, const float2* __restrict__ tw, int tid) {
+  NoIO io;
+  fft_pow2_io<INV, N, T, false, true, true>(lds, tw, tid, io, io);
 }
 
 // Full transform of one row held in LDS (natural order in and out).  Unnormalised.
