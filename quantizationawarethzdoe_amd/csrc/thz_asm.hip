@@ -36,6 +36,7 @@ struct AsmArgs {
   int in_r0, in_c0, Hin, Win;     // input window inside the padded plane
   int out_r0, out_c0, Hout, Wout; // output window
   int ncols, J;                   // kept spectral columns, m_y = c - J
+  int ncb;                        // column blocks of CB columns (blocked T / U layout)
   int nz, zoff;                   // z-planes in this chunk, offset into zv
   int bl, adjoint;
   float dx, dy, scale;
@@ -50,6 +51,26 @@ __device__ __forceinline__ int xcd_rows(int b, int nb) {
   if (nb & 127) return b;
   const int xcd = b & 7, slot = b >> 3;
   return (((slot >> 4) << 3) + xcd) * 16 + (slot & 15);
+}
+
+// Contiguous chunk of block ids per XCD (the bijective form of cdna_hip_programming.md §5):
+// consecutive logical ids land on one XCD and start close together in time.  Speed only.
+__device__ __forceinline__ int xcd_chunk(int b, int nb) {
+  const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// Blocked column-major layout of the spectral intermediates T and U: element (c, row) of a
+// plane lives at ((cb * rows + row) * CB + c % CB), cb = c / CB.  A row pass then touches CB
+// consecutive columns as one 128-B segment (K1 stores, K3 gathers), and the column pass
+// touches one 8-B element per segment; the CB column workgroups sharing a segment run on
+// one XCD back to back (xcd_chunk) so the L2 merges their partial lines.
+#ifndef THZ_CB
+#define THZ_CB 16
+#endif
+constexpr int CB = THZ_CB;
+__device__ __forceinline__ size_t blk(int c, int row, int rows) {
+  return ((size_t)(c / CB) * rows + row) * CB + (c % CB);
 }
 
 __device__ __forceinline__ int freq_index(int i, int n) { return i < n - n / 2 ? i : i - n; }
@@ -159,7 +180,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
   const int bc = row / a.Hin, h = row - bc * a.Hin;
   const int tid = threadIdx.x, nt = blockDim.x;
   const float2* src = in + ((size_t)bc * a.Hin + h) * a.Win;
-  float2* dst = T + (size_t)bc * a.ncols * a.Hin + h;
+  float2* dst = T + (size_t)bc * a.ncb * CB * a.Hin;
   if constexpr (PN > 0) {
     auto ld = [&](int, int, int idx) {
       const int s = idx - a.in_c0;
@@ -167,7 +188,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int c = band_col(j, PN, a.J, a.ncols);
-      if (c >= 0) dst[(size_t)c * a.Hin] = v;
+      if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
     fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
   } else {
@@ -180,7 +201,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
     for (int c = tid; c < a.ncols; c += nt) {
       int j = c - a.J;
       if (j < 0) j += a.Pw;
-      dst[(size_t)c * a.Hin] = lds[padx(j)];
+      dst[blk(c, h, a.Hin)] = lds[padx(j)];
     }
   }
 }
@@ -192,10 +213,11 @@ template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   extern __shared__ float2 lds[];
-  const int c = blockIdx.x, bc = blockIdx.y;
+  const int id = xcd_chunk(blockIdx.x, gridDim.x);
+  const int bc = id / a.ncols, c = id - bc * a.ncols;
   const int nt = blockDim.x;
   const int Ph = a.Ph;
-  const float2* col = T + ((size_t)bc * a.ncols + c) * a.Hin;
+  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
   const float lam = a.lam[bc % a.C];
   const float Ky = kfreq(c - a.J, a.Pw, a.dy);
   // Each phase works from its own opaque copy of threadIdx.x: otherwise the compiler CSEs /
@@ -210,7 +232,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
     float2 sp[MBL][RL];                              // spectrum, element i + r*PN/RL
     auto ld0 = [&](int, int, int idx) {
       const int s = idx - a.in_r0;
-      return (s >= 0 && s < a.Hin) ? col[s] : make_float2(0.f, 0.f);
+      return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
     fft_pow2_io<false, PN, TT, false, false, false>(lds, ph.tw, tid, ld0, sv0);
@@ -223,17 +245,17 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       auto ld1 = [&](int m, int r, int idx) {
         return cmul(sp[m][r], tf_value(a, s, kfreq(freq_index(idx, PN), PN, a.dx), Ky));
       };
-      float2* dst = U + (((size_t)zz * a.BC + bc) * a.ncols + c) * a.Hout;
+      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if (r >= 0 && r < a.Hout) dst[r] = cscale(v, a.scale);
+        if (r >= 0 && r < a.Hout) dst[(size_t)r * CB] = cscale(v, a.scale);
       };
       fft_pow2_io<true, PN, TT, true, false, false>(lds, ph.tw, tz, ld1, sv1);
     }
   } else {
     for (int i = tid; i < Ph; i += nt) {
       const int s = i - a.in_r0;
-      lds[padx(i)] = (s >= 0 && s < a.Hin) ? col[s] : make_float2(0.f, 0.f);
+      lds[padx(i)] = (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
     }
     __syncthreads();
     fft_lds<false>(lds, ph, tid, nt);
@@ -256,8 +278,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       }
       __syncthreads();
       fft_lds<true>(lds, ph, tm, nt);
-      float2* dst = U + (((size_t)zz * a.BC + bc) * a.ncols + c) * a.Hout;
-      for (int r = tm; r < a.Hout; r += nt) dst[r] = cscale(lds[padx(a.out_r0 + r)], a.scale);
+      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
+      for (int r = tm; r < a.Hout; r += nt) dst[(size_t)r * CB] = cscale(lds[padx(a.out_r0 + r)], a.scale);
     }
   }
 }
@@ -272,12 +294,12 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   const int row = xcd_rows(blockIdx.x, gridDim.x);  // row in [0, nz*BC*Hout)
   const int plane = row / a.Hout, r = row - plane * a.Hout;  // plane = zz*BC + bc
   const int tid = threadIdx.x, nt = blockDim.x;
-  const float2* src = U + (size_t)plane * a.ncols * a.Hout + r;
+  const float2* src = U + (size_t)plane * a.ncb * CB * a.Hout;
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
   if constexpr (PN > 0) {
     auto ld = [&](int, int, int j) {
       const int c = band_col(j, PN, a.J, a.ncols);
-      return c >= 0 ? src[(size_t)c * a.Hout] : make_float2(0.f, 0.f);
+      return c >= 0 ? src[blk(c, r, a.Hout)] : make_float2(0.f, 0.f);
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int w = j - a.out_c0;
@@ -287,7 +309,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);
-      lds[padx(j)] = c >= 0 ? src[(size_t)c * a.Hout] : make_float2(0.f, 0.f);
+      lds[padx(j)] = c >= 0 ? src[blk(c, r, a.Hout)] : make_float2(0.f, 0.f);
     }
     __syncthreads();
     fft_lds<true>(lds, pw, tid, nt);
@@ -322,7 +344,7 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
 // Host side
 // ---------------------------------------------------------------------------------------------
 struct AsmGeom {
-  int BC, Ph, Pw, ncols, J, Hin, Win, Hout, Wout, zc;
+  int BC, Ph, Pw, ncols, J, ncb, Hin, Win, Hout, Wout, zc;
 };
 
 static int validate(const thz_asm_desc* d) {
@@ -392,12 +414,13 @@ static void geometry(const thz_asm_desc* d, AsmGeom* g) {
     g->ncols = 2 * J + 1;
     g->J = J;
   }
+  g->ncb = (g->ncols + CB - 1) / CB;
   int zc = d->z_chunk > 0 ? d->z_chunk : 0;
   if (zc == 0) {
     // default: up to 16 z-planes per column pass (the forward column FFT and the T read are
     // shared by the chunk), U capped at 2.5 GiB of the 288 GB HBM.  Measured on cfg2:
     // z_chunk 1/4/8/16 -> 2006/2620/2753/2859 planes/s.
-    const double per_z = (double)g->BC * g->ncols * g->Hout * sizeof(float2);
+    const double per_z = (double)g->BC * g->ncb * CB * g->Hout * sizeof(float2);
     zc = (int)std::max(1.0, std::min(16.0, std::floor((2560.0 * 1024 * 1024) / per_z)));
   }
   g->zc = std::min(zc, d->adjoint ? 1 : d->Z);
@@ -456,8 +479,8 @@ static int ensure_lds_attr() {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static size_t ws_bytes(const AsmGeom& g) {
-  return align256((size_t)g.BC * g.ncols * g.Hin * sizeof(float2)) +
-         align256((size_t)g.zc * g.BC * g.ncols * g.Hout * sizeof(float2));
+  return align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)) +
+         align256((size_t)g.zc * g.BC * g.ncb * CB * g.Hout * sizeof(float2));
 }
 
 }  // namespace thz
@@ -513,6 +536,7 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
     a.out_r0 = d->pad_h; a.out_c0 = d->pad_w; a.Hout = d->H; a.Wout = d->W;
   }
   a.ncols = g.ncols;
+  a.ncb = g.ncb;
   a.J = g.J;
   a.bl = d->bandlimit;
   a.adjoint = d->adjoint;
@@ -525,7 +549,7 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
   hipStream_t s = (hipStream_t)stream;
   if ((e = ensure_lds_attr())) return e;
   float2* T = (float2*)workspace;
-  float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncols * g.Hin * sizeof(float2)));
+  float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
   const int tw = threads_for(g.Pw), th = threads_for(g.Ph);
 
   {
@@ -540,7 +564,7 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
     a.nz = std::min(g.zc, d->Z - z0);
     {
       KernelTimer kt("asm_cols", s);
-      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols, g.BC), dim3(th), fft_lds_bytes(g.Ph), s, (const float2*)T, U,
+      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols * g.BC), dim3(th), fft_lds_bytes(g.Ph), s, (const float2*)T, U,
                       ph, a);
       THZ_LAUNCH_CHECK();
       kt.stop();
