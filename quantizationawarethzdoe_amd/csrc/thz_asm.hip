@@ -132,6 +132,29 @@ __device__ __forceinline__ void sincos_rad(float ang, float* sn, float* cs) {
 }
 
 __device__ __forceinline__ float kfreq(int m, int P, float d) { return (TWO_PI_F * ((float)m / (float)P)) / d; }
+// single IEEE operations that must not be fused with neighbours (contraction is off here)
+__device__ __forceinline__ float tf_mul(float x, float y) { return x * y; }
+__device__ __forceinline__ float tf_add(float x, float y) { return x + y; }
+__device__ __forceinline__ float tf_sub(float x, float y) { return x - y; }
+__device__ __forceinline__ float tf_div(float x, float y) { return x / y; }
+
+
+
+// Mask of H at spectral row m (Kx = kfreq(m)) for the column Ky: exactly the tests of
+// tf_value below, in the same fp32 operation order.
+__device__ __forceinline__ bool tf_pass(int bl, int Ph, float dx, const TfScalars& s, float Ky, int m) {
+  const float Kx = kfreq(m, Ph, dx);
+  const float Kx2 = Kx * Kx, Ky2 = Ky * Ky;
+  const float d = s.kl2 - (Kx2 + Ky2);
+  if (d < 0.0f) return false;
+  if (bl == THZ_BANDLIMIT_EXACT) {
+    const bool c1 = (Kx2 / s.A + Ky2 / s.kl2) <= 1.0f;
+    const bool c2 = (Kx2 / s.kl2 + Ky2 / s.Bv) <= 1.0f;
+    return c1 && c2;
+  }
+  if (bl == THZ_BANDLIMIT_APPROX) return !(fabsf(Kx) > s.kxm || fabsf(Ky) > s.kym);
+  return true;
+}
 
 // H(kx, ky) = exp(i z sqrt(k^2 - K^2)) with the evanescent and band-limit masks
 // (Props/ASM_Prop.py:245-306).  conj for the adjoint.
@@ -236,14 +259,54 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
     fft_pow2_io<false, PN, TT, false, false, false>(lds, ph.tw, tid, ld0, sv0);
+    // The evanescent and band-limit masks are monotone in |m_x| (every fp32 operation of
+    // Props/ASM_Prop.py:245-306 is monotone), so for each z the kept rows of this column are
+    // exactly |m_x| <= M_z.  One lane per z finds M_z by bisection with the exact
+    // reference-order tests; the per-element work is then sqrt once per column and one
+    // sincos per z.
+    int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN));
+    const float kl = TWO_PI_F / lam;
+    const float kl2 = tf_mul(kl, kl);
+    const float Ky2 = tf_mul(Ky, Ky);
+    if ((int)threadIdx.x < a.nz) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + threadIdx.x]);
+      int lo = -1, hi = PN / 2 + 1;
+      const int bl = a.bl, P = a.Ph;
+      const float dx = a.dx;
+      if (tf_pass(bl, P, dx, s, Ky, 0)) {
+        lo = 0;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (tf_pass(bl, P, dx, s, Ky, mid)) lo = mid;
+          else hi = mid;
+        }
+      }
+      mz[threadIdx.x] = lo;
+    }
+    float sq[MBL][RL];
+    asm volatile("" : "+v"(tid));
+#pragma unroll
+    for (int m = 0; m < MBL; ++m)
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        const float Kx = kfreq(freq_index(tid + m * TT + r * (PN / RL), PN), PN, a.dx);
+        const float d = tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2));
+        sq[m][r] = sqrtf(fmaxf(d, 0.0f));
+      }
+    __syncthreads();  // mz visible
     for (int zz = 0; zz < a.nz; ++zz) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      const float z = a.zv[a.zoff + zz];
+      const int M = mz[zz];
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
       auto ld1 = [&](int m, int r, int idx) {
-        return cmul(sp[m][r], tf_value(a, s, kfreq(freq_index(idx, PN), PN, a.dx), Ky));
+        const int mx = freq_index(idx, PN);
+        if (mx > M || -mx > M) return make_float2(0.f, 0.f);
+        float sn, cs;
+        sincos_rad(tf_mul(z, sq[m][r]), &sn, &cs);
+        return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
       };
       float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
@@ -458,7 +521,7 @@ static int ensure_lds_attr() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
-    const int mx = (int)fft_lds_bytes(FFT_MAX_N);
+    const int mx = (int)fft_lds_bytes(FFT_MAX_N) + 4 * THZ_MAX_Z;
     std::vector<const void*> ks;
     add_kernels<0>(ks);
     add_kernels<1024>(ks);
@@ -564,7 +627,7 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
     a.nz = std::min(g.zc, d->Z - z0);
     {
       KernelTimer kt("asm_cols", s);
-      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols * g.BC), dim3(th), fft_lds_bytes(g.Ph), s, (const float2*)T, U,
+      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols * g.BC), dim3(th), fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z, s, (const float2*)T, U,
                       ph, a);
       THZ_LAUNCH_CHECK();
       kt.stop();
