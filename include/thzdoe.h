@@ -19,6 +19,7 @@
  *
  * Reference interfaces replaced (paths relative to the reference repo root):
  *   thz_asm_*        Props/ASM_Prop.py:17-378    ASM_prop.forward (+ autograd adjoint)
+ *   thz_czt_*        Props/CZT_Prop.py:11-314    CZT_prop.forward / VCZT_prop
  *   thz_fft_*        utils/Helper_Functions.py:99-160 ft2/ift2 (centred ortho FFT)
  */
 #ifndef THZDOE_H_
@@ -79,6 +80,28 @@ int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* work
 /* Plan facts for diagnostics / bench byte counts: number of spectral columns the kernels
  * keep (|m_y| <= J; ncols = 2J+1, or Pw when nothing is cut) and z-planes per column pass. */
 int thz_asm_band(const thz_asm_desc* d, int* ncols, int* z_chunk);
+
+/*
+ * Chirp-z (Bluestein) Rayleigh-Sommerfeld propagation with output zoom,
+ * Props/CZT_Prop.py:252-314 (forward).
+ *   in  [B, C, H, W] complex64, spacing (dx, dy)
+ *   out [B, C, outW, outH] (the reference's transposed result; outH must equal outW,
+ *        as the reference's final F0 * U broadcast requires, :248)
+ * wavelengths[C] host floats; z, output spacing (odx, ody) as in forward(field, outputHeight,
+ * outputWidth, outputPixel_dx, outputPixel_dy).
+ */
+typedef struct thz_czt_desc {
+  int B, C, H, W;
+  int outH, outW;
+  float dx, dy;
+  float odx, ody;
+  float z;
+  const float* wavelengths; /* host [C] */
+} thz_czt_desc;
+
+int thz_czt_workspace_size(const thz_czt_desc* d, size_t* bytes);
+int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
+                    thz_stream_t stream);
 
 /*
  * Batched 1-D FFT along the contiguous axis (the building block of ft2/ift2,

@@ -27,6 +27,7 @@ BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 EXPORTED = [
     "thz_version", "thz_last_error",
     "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band",
+    "thz_czt_workspace_size", "thz_czt_forward",
     "thz_fft_rows",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
@@ -51,6 +52,15 @@ class AsmDesc(ctypes.Structure):
     ]
 
 
+class CztDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("outH", ctypes.c_int), ("outW", ctypes.c_int),
+        ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("odx", ctypes.c_float), ("ody", ctypes.c_float),
+        ("z", ctypes.c_float), ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -63,6 +73,8 @@ def _declare(lib):
     lib.thz_asm_forward.argtypes = [ctypes.POINTER(AsmDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_asm_band.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
     lib.thz_fft_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+    lib.thz_czt_workspace_size.argtypes = [ctypes.POINTER(CztDesc), ctypes.POINTER(c_size_t)]
+    lib.thz_czt_forward.argtypes = [ctypes.POINTER(CztDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]
     lib.thz_timing_reset.argtypes = []
     lib.thz_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]

@@ -1,0 +1,434 @@
+// Chirp-z (Bluestein) Rayleigh-Sommerfeld propagation with output zoom, CZT_prop
+// (Props/CZT_Prop.py:11-314), for gfx950.
+//
+// Reference sequence (per wavelength c, Dm = lambda z / dx_in):
+//   U0 = E * F(x_in, y_in)                                   RS kernel, :44-57, :238
+//   U1 = Bluestein(U0, axis H, fy1, fy2, M = outW)           :243  (output transposed)
+//   U2 = Bluestein(U1, axis W, fx1, fx2, M = outH)           :246
+//   out = F0(x_out, y_out) * U2 * z * dxo * dyo * lambda     :248
+// Bluestein (:132-225): x * A^-j * h[m-1+j] -> FFT_np2 -> * FFT_np2(1/h[0:mp+1]) -> IFFT ->
+// rows [m, m+M) -> * h[m-1+l] * M_shift[l], h[t] = W^((t-m+1)^2/2), np2 = 2^ceil(log2(m+M-1)).
+//
+// The two 1-D transforms act on different axes, so they commute; this build runs the W
+// axis first over contiguous rows (pass A, params fx / outH) and the H axis second over the
+// blocked-column intermediate (pass B, params fy / outW), producing the reference's
+// [B, C, outW, outH] result.  Each pass is one kernel: fused-I/O forward FFT (input chirp and
+// RS kernel applied in the first-stage loader), spectrum kept in registers, filter multiply
+// in the inverse's first-stage loader, output chirp / M_shift (and F0 for pass B) applied in
+// the last-stage storer.  The chirp tables are generated on the device in DOUBLE precision
+// (the reference's fp32 complex pow is its dominant error), the filter
+// spectra by the same LDS FFT.
+#include <algorithm>
+#include <cmath>
+#include <mutex>
+
+#include "thz_common.hpp"
+#include "thz_dev.hpp"
+
+namespace thz {
+
+struct BluePass {
+  int m, M, np2;
+  int ntab;        // length of the 1/h sequence actually used: min(mp + 1, Lh)
+  double f1, f2;   // frequency range
+};
+
+struct CztArgs {
+  int BC, C, H, W, outH, outW;
+  float dx, dy, odx, ody, z;
+  BluePass pa, pb;   // pass A: W axis (fx, outH); pass B: H axis (fy, outW)
+  int ncbA;          // column blocks of the intermediate V (outH columns)
+  // table offsets (in float2) inside the workspace, per wavelength stride
+  size_t preA, postA, ftA, preB, postB, ftB, tabStride;
+  float lam[THZ_MAX_WAVELENGTHS];
+};
+
+// --------------------------------------------------------------------------------------------
+// Bluestein parameters in double from the fp32-rounded inputs (Props/CZT_Prop.py:109-116,
+// 179-225).
+// --------------------------------------------------------------------------------------------
+struct BlueD {
+  double Dm, D1, D2, thA, thW;
+};
+
+__device__ __forceinline__ BlueD blue_params(const BluePass& p, double lam, double z, double dx) {
+  BlueD b;
+  b.Dm = lam * z / dx;
+  const double f1 = p.f1 + b.Dm / 2, f2 = p.f2 + b.Dm / 2;
+  const double M = p.M;
+  b.D1 = f1 + (M * b.Dm + f2 - f1) / (2 * M);
+  b.D2 = f2 + (M * b.Dm + f2 - f1) / (2 * M);
+  const double twopi = 6.283185307179586476925;
+  b.thA = twopi * b.D1 / b.Dm;
+  b.thW = -twopi * (b.D1 - b.D2) / (M * b.Dm);
+  return b;
+}
+
+// Tables for one pass and one wavelength: pre[j] = A^-j W^(j^2/2), post[l] = W^(l^2/2) *
+// M_shift[l] / np2 (the unnormalised inverse FFT's 1/np2 folded in), g[t] = 1/h[t] (FFT'd
+// in place afterwards into the filter spectrum).
+__global__ void czt_tables(CztArgs a, float2* __restrict__ ws, int pass) {
+  const int c = blockIdx.y;
+  const BluePass& p = pass == 0 ? a.pa : a.pb;
+  const BlueD b = blue_params(p, (double)a.lam[c], (double)a.z, (double)a.dx);
+  float2* pre = ws + (pass == 0 ? a.preA : a.preB) + (size_t)c * a.tabStride;
+  float2* post = ws + (pass == 0 ? a.postA : a.postB) + (size_t)c * a.tabStride;
+  float2* g = ws + (pass == 0 ? a.ftA : a.ftB) + (size_t)c * a.tabStride;
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < p.m) {
+    const double j = n;
+    pre[n] = cis_d(-b.thA * j + b.thW * j * j / 2);
+  }
+  if (n < p.M) {
+    const double l = n;
+    const double ell = l / p.M * (b.D2 - b.D1) + b.D1;
+    const double shift = -6.283185307179586476925 * ell * (-p.m / 2.0 + 0.5) / b.Dm;
+    const float2 v = cis_d(b.thW * l * l / 2 + shift);
+    const float s = 1.0f / (float)p.np2;
+    post[n] = make_float2(v.x * s, v.y * s);
+  }
+  if (n < p.np2) {
+    if (n < p.ntab) {
+      const double jj = n - p.m + 1;
+      g[n] = cis_d(-b.thW * jj * jj / 2);
+    } else {
+      g[n] = make_float2(0.f, 0.f);
+    }
+  }
+}
+
+// RS kernel exp(ikr) z/(2 pi r^2) (1/r - ik) (Props/CZT_Prop.py:44-57).  The amplitude is
+// fp32 in the reference's operation order; the phase k r (thousands of radians) is formed as
+// (k|z| mod 2 pi, from double) + k rho^2 / (r + |z|) -- the exact identity r - |z| =
+// rho^2/(r + |z|) keeps the fp32 part small, so the phase error drops from ~2e-4 rad (fp32
+// k*r, which the reference pays and which costs it ~4e-3 rel-L2 on the test_czt.py case)
+// to ~3e-5 rad.
+struct RsPhase {
+  float kzmod;  // (k |z|) mod 2 pi, k = 2 pi / lambda, evaluated in double
+  float k;
+};
+__device__ __forceinline__ RsPhase rs_phase(float lam, float z) {
+  const double k = 6.283185307179586476925 / (double)lam;
+  double kz = k * fabs((double)z);
+  kz -= 6.283185307179586476925 * floor(kz / 6.283185307179586476925);
+  RsPhase p;
+  p.kzmod = (float)kz;
+  p.k = (float)k;
+  return p;
+}
+
+#pragma clang fp contract(off)
+__device__ __forceinline__ float2 rs_kernel(float x, float y, float z, float k, const RsPhase& ph) {
+  const float rho2 = x * x + y * y;
+  const float r = sqrtf(rho2 + z * z);
+  const float f = 0.15915494309189535f * z / (r * r);
+  const float fr = f * (1.0f / r), fi = -(f * k);
+  float sn, cs;
+  sincos_rad(ph.kzmod + ph.k * (rho2 / (r + fabsf(z))), &sn, &cs);
+  return make_float2(cs * fr - sn * fi, cs * fi + sn * fr);
+}
+
+// torch.linspace(start, end, n)[i] in fp32 (symmetric two-sided form of ATen's CPU kernel)
+__device__ __forceinline__ float lin(float start, float end, int n, int i) {
+  if (n == 1) return start;
+  const float step = (end - start) / (float)(n - 1);
+  const int half = n / 2;
+  return i < half ? start + step * (float)i : end - step * (float)(n - 1 - i);
+}
+#pragma clang fp contract(on)
+
+template <int PN>
+struct CztGeo {
+  static constexpr int T = PN > 0 ? PN / FFT_MAXV : 0;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Pass A: rows (W axis).  in [BC][H][W] -> V blocked [BC][q/16][h][16], q in [0, outH)
+// ---------------------------------------------------------------------------------------------
+template <int PN>
+__global__ void __launch_bounds__(1024) czt_rows(const float2* __restrict__ in, float2* __restrict__ V,
+                                                const float2* __restrict__ ws, FftPlan pl, CztArgs a) {
+  extern __shared__ float2 lds[];
+  const int row = blockIdx.x;
+  const int bc = row / a.H, h = row - bc * a.H;
+  const int c = bc % a.C;
+  const float lam = a.lam[c];
+  const float k = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, a.z);
+  const float xh = lin(-(float)a.H * a.dx / 2.0f, (float)a.H * a.dx / 2.0f, a.H, h);
+  const float2* src = in + ((size_t)bc * a.H + h) * a.W;
+  const float2* pre = ws + a.preA + (size_t)c * a.tabStride;
+  const float2* post = ws + a.postA + (size_t)c * a.tabStride;
+  const float2* ft = ws + a.ftA + (size_t)c * a.tabStride;
+  float2* dst = V + (size_t)bc * a.ncbA * CB * a.H;
+  const int m = a.W, M = a.outH;
+  const float ylo = -(float)a.W * a.dy / 2.0f, yhi = (float)a.W * a.dy / 2.0f;
+  auto load_x = [&](int w) {
+    if (w >= m) return make_float2(0.f, 0.f);
+    const float2 F = rs_kernel(xh, lin(ylo, yhi, a.W, w), a.z, k, rph);
+    return cmul(cmul(src[w], F), pre[w]);
+  };
+  auto store_y = [&](int j, float2 v) {
+    const int q = j - m;
+    if (q >= 0 && q < M) dst[blk(q, h, a.H)] = cmul(v, post[q]);
+  };
+  int tid = threadIdx.x;
+  if constexpr (PN > 0) {
+    using S = Pow2Sched<PN>;
+    constexpr int TT = CztGeo<PN>::T;
+    constexpr int RL = S::radix(S::NST - 1, false);
+    constexpr int MBL = PN / RL / TT;
+    float2 sp[MBL][RL];
+    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
+    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, pl.tw, tid, ld0, sv0);
+    asm volatile("" : "+v"(tid));
+    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
+    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
+    fft_pow2_io<true, PN, TT, true, false, false>(lds, pl.tw, tid, ld1, sv1);
+  } else {
+    const int n = pl.n, nt = blockDim.x;
+    for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
+    __syncthreads();
+    fft_lds<false>(lds, pl, tid, nt);
+    for (int j = tid; j < n; j += nt) lds[padx(j)] = cmul(lds[padx(j)], ft[j]);
+    __syncthreads();
+    fft_lds<true>(lds, pl, tid, nt);
+    for (int j = tid; j < n; j += nt) store_y(j, lds[padx(j)]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pass B: columns (H axis) of V.  -> out [BC][outW][outH]: out[p][q] = F0 * U * z dxo dyo lambda
+// ---------------------------------------------------------------------------------------------
+template <int PN>
+__global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, float2* __restrict__ out,
+                                                const float2* __restrict__ ws, FftPlan pl, CztArgs a) {
+  extern __shared__ float2 lds[];
+  const int id = xcd_chunk(blockIdx.x, gridDim.x);
+  const int bc = id / a.outH, q = id - bc * a.outH;
+  const int c = bc % a.C;
+  const float lam = a.lam[c];
+  const float k = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, a.z);
+  const float2* col = V + (size_t)bc * a.ncbA * CB * a.H + blk(q, 0, a.H);
+  const float2* pre = ws + a.preB + (size_t)c * a.tabStride;
+  const float2* post = ws + a.postB + (size_t)c * a.tabStride;
+  const float2* ft = ws + a.ftB + (size_t)c * a.tabStride;
+  float2* dst = out + (size_t)bc * a.outW * a.outH + q;
+  const int m = a.H, M = a.outW;
+  // F0 on the output mesh: Outmeshx[p][q] = x_out[p] (outH, dxo), Outmeshy = y_out[q] (outW, dyo)
+  const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
+  const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
+  const float cst = ((a.z * a.odx) * a.ody) * lam;
+  auto load_x = [&](int h) { return h < m ? cmul(col[(size_t)h * CB], pre[h]) : make_float2(0.f, 0.f); };
+  auto store_y = [&](int j, float2 v) {
+    const int p = j - m;
+    if (p >= 0 && p < M) {
+      const float2 F0 = rs_kernel(lin(xlo, xhi, a.outH, p), yq, a.z, k, rph);
+      dst[(size_t)p * a.outH] = cscale(cmul(F0, cmul(v, post[p])), cst);
+    }
+  };
+  int tid = threadIdx.x;
+  if constexpr (PN > 0) {
+    using S = Pow2Sched<PN>;
+    constexpr int TT = CztGeo<PN>::T;
+    constexpr int RL = S::radix(S::NST - 1, false);
+    constexpr int MBL = PN / RL / TT;
+    float2 sp[MBL][RL];
+    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
+    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, pl.tw, tid, ld0, sv0);
+    asm volatile("" : "+v"(tid));
+    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
+    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
+    fft_pow2_io<true, PN, TT, true, false, false>(lds, pl.tw, tid, ld1, sv1);
+  } else {
+    const int n = pl.n, nt = blockDim.x;
+    for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
+    __syncthreads();
+    fft_lds<false>(lds, pl, tid, nt);
+    for (int j = tid; j < n; j += nt) lds[padx(j)] = cmul(lds[padx(j)], ft[j]);
+    __syncthreads();
+    fft_lds<true>(lds, pl, tid, nt);
+    for (int j = tid; j < n; j += nt) store_y(j, lds[padx(j)]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------------
+static int np2_of(int x) {
+  int p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+static void make_pass(BluePass* p, int m, int M, double lo, double hi) {
+  p->m = m;
+  p->M = M;
+  const int mp = m + M - 1;
+  p->np2 = np2_of(mp);
+  const int Lh = m + std::max(M - 1, m - 1);  // arange(-m+1, max(M-1, m-1)+1)
+  p->ntab = std::min(mp + 1, Lh);
+  p->f1 = lo;
+  p->f2 = hi;
+}
+
+static int czt_validate(const thz_czt_desc* d) {
+  if (!d) return fail(THZ_E_ARG, "null descriptor");
+  if (d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1 || d->outH < 1 || d->outW < 1)
+    return fail(THZ_E_ARG, "bad CZT shape");
+  if (d->outH != d->outW)
+    return fail(THZ_E_ARG, "CZT output must be square: the reference multiplies F0 [outH,outW] with the "
+                           "transposed [outW,outH] transform (Props/CZT_Prop.py:248); got %dx%d",
+                d->outH, d->outW);
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  if (!d->wavelengths) return fail(THZ_E_ARG, "null wavelengths");
+  const int nA = np2_of(d->W + d->outH - 1), nB = np2_of(d->H + d->outW - 1);
+  if (nA > FFT_MAX_N || nB > FFT_MAX_N)
+    return fail(THZ_E_UNSUPPORTED, "Bluestein length %d/%d exceeds %d", nA, nB, FFT_MAX_N);
+  return THZ_OK;
+}
+
+static size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+static void czt_layout(const thz_czt_desc* d, CztArgs* a, size_t* total) {
+  a->BC = d->B * d->C;
+  a->C = d->C;
+  a->H = d->H;
+  a->W = d->W;
+  a->outH = d->outH;
+  a->outW = d->outW;
+  a->dx = d->dx;
+  a->dy = d->dy;
+  a->odx = d->odx;
+  a->ody = d->ody;
+  a->z = d->z;
+  // x_out = linspace(-outH dxo/2, outH dxo/2, outH), y_out likewise (Props/CZT_Prop.py:101-102)
+  const double xo = (double)(float)((float)d->outH * d->odx / 2.0f);
+  const double yo = (double)(float)((float)d->outW * d->ody / 2.0f);
+  make_pass(&a->pa, d->W, d->outH, -xo, xo);  // second reference Bluestein (:246): fx, outH
+  make_pass(&a->pb, d->H, d->outW, -yo, yo);  // first reference Bluestein (:243): fy, outW
+  a->ncbA = (d->outH + CB - 1) / CB;
+  size_t off = 0;
+  auto take = [&](size_t n) {
+    size_t o = off;
+    off += (n + 31) & ~(size_t)31;
+    return o;
+  };
+  a->preA = take(a->pa.m);
+  a->postA = take(a->pa.M);
+  a->ftA = take(a->pa.np2);
+  a->preB = take(a->pb.m);
+  a->postB = take(a->pb.M);
+  a->ftB = take(a->pb.np2);
+  a->tabStride = off;
+  for (int c = 0; c < d->C; ++c) a->lam[c] = d->wavelengths[c];
+  const size_t tab = a256((size_t)a->tabStride * d->C * sizeof(float2));
+  const size_t vbytes = a256((size_t)a->BC * a->ncbA * CB * d->H * sizeof(float2));
+  *total = tab + vbytes;
+}
+
+static int czt_pow2(int n) {
+  switch (n) {
+    case 1024: case 2048: case 4096: case 8192: case 16384: return n;
+    default: return 0;
+  }
+}
+
+#define THZ_CZT_SWITCH(n, KER, ...)                                                     \
+  switch (czt_pow2(n)) {                                                                 \
+    case 1024: hipLaunchKernelGGL(KER<1024>, __VA_ARGS__); break;                        \
+    case 2048: hipLaunchKernelGGL(KER<2048>, __VA_ARGS__); break;                        \
+    case 4096: hipLaunchKernelGGL(KER<4096>, __VA_ARGS__); break;                        \
+    case 8192: hipLaunchKernelGGL(KER<8192>, __VA_ARGS__); break;                        \
+    case 16384: hipLaunchKernelGGL(KER<16384>, __VA_ARGS__); break;                      \
+    default: hipLaunchKernelGGL(KER<0>, __VA_ARGS__); break;                             \
+  }
+
+static int czt_lds_attr() {
+  static std::once_flag once;
+  static hipError_t err = hipSuccess;
+  std::call_once(once, [] {
+    const int mx = (int)fft_lds_bytes(FFT_MAX_N);
+    const void* ks[] = {
+        (const void*)czt_rows<0>,     (const void*)czt_rows<1024>, (const void*)czt_rows<2048>,
+        (const void*)czt_rows<4096>,  (const void*)czt_rows<8192>, (const void*)czt_rows<16384>,
+        (const void*)czt_cols<0>,     (const void*)czt_cols<1024>, (const void*)czt_cols<2048>,
+        (const void*)czt_cols<4096>,  (const void*)czt_cols<8192>, (const void*)czt_cols<16384>};
+    for (const void* k : ks) {
+      hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
+      if (e != hipSuccess) err = e;
+    }
+  });
+  if (err != hipSuccess) return fail(THZ_E_HIP, "hipFuncSetAttribute: %s", hipGetErrorString(err));
+  return THZ_OK;
+}
+
+static int threads_pow2_or(int n) { return czt_pow2(n) ? n / FFT_MAXV : fft_threads(n); }
+
+}  // namespace thz
+
+using namespace thz;
+
+extern "C" int thz_czt_workspace_size(const thz_czt_desc* d, size_t* bytes) {
+  int e = czt_validate(d);
+  if (e) return e;
+  if (!bytes) return fail(THZ_E_ARG, "null bytes");
+  CztArgs a;
+  czt_layout(d, &a, bytes);
+  return THZ_OK;
+}
+
+extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out, void* workspace,
+                               size_t workspace_bytes, thz_stream_t stream) {
+  int e = czt_validate(d);
+  if (e) return e;
+  if (!in || !out) return fail(THZ_E_ARG, "null data pointer");
+  CztArgs a{};
+  size_t need = 0;
+  czt_layout(d, &a, &need);
+  if (!workspace || workspace_bytes < need)
+    return fail(THZ_E_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+  if ((e = czt_lds_attr())) return e;
+  FftPlan plA, plB;
+  if ((e = get_plan(a.pa.np2, &plA))) return e;
+  if ((e = get_plan(a.pb.np2, &plB))) return e;
+  hipStream_t s = (hipStream_t)stream;
+  float2* ws = (float2*)workspace;
+  float2* V = (float2*)((char*)workspace + a256((size_t)a.tabStride * d->C * sizeof(float2)));
+  {
+    KernelTimer kt("czt_tables", s);
+    const int nA = std::max({a.pa.m, a.pa.M, a.pa.np2}), nB = std::max({a.pb.m, a.pb.M, a.pb.np2});
+    hipLaunchKernelGGL(czt_tables, dim3((nA + 255) / 256, d->C), dim3(256), 0, s, a, ws, 0);
+    THZ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(czt_tables, dim3((nB + 255) / 256, d->C), dim3(256), 0, s, a, ws, 1);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  // filter spectra FFT_np2(1/h) in place, one row per wavelength
+  for (int c = 0; c < d->C; ++c) {
+    if ((e = thz_fft_rows(ws + a.ftA + (size_t)c * a.tabStride, ws + a.ftA + (size_t)c * a.tabStride, 1,
+                          a.pa.np2, 0, stream)))
+      return e;
+    if ((e = thz_fft_rows(ws + a.ftB + (size_t)c * a.tabStride, ws + a.ftB + (size_t)c * a.tabStride, 1,
+                          a.pb.np2, 0, stream)))
+      return e;
+  }
+  {
+    KernelTimer kt("czt_rows", s);
+    THZ_CZT_SWITCH(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
+                   fft_lds_bytes(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  {
+    KernelTimer kt("czt_cols", s);
+    THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
+                   fft_lds_bytes(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  return THZ_OK;
+}

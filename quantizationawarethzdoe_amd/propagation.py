@@ -125,3 +125,26 @@ def fft_rows(x, inverse=False):
         _lib.check(_lib.lib().thz_fft_rows(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                                            rows, n, int(inverse), _stream_handle()))
     return out
+
+
+def czt_apply(data, wavelengths, spacing, z, outH, outW, odx, ody):
+    """Chirp-z propagation [B,C,H,W] -> [B,C,outW,outH] (Props/CZT_Prop.py:252-314) on the HIP kernels."""
+    _require_device(data, "CZT")
+    if data.dtype != torch.complex64:
+        raise TypeError(f"CZT kernels compute in complex64; got {data.dtype}")
+    data = data.contiguous()
+    B, C, H, W = data.shape
+    wl = _lib.float_array(wavelengths)
+    d = _lib.CztDesc(B=B, C=C, H=H, W=W, outH=int(outH), outW=int(outW), dx=float(spacing[0]),
+                     dy=float(spacing[1]), odx=float(odx), ody=float(ody), z=float(z),
+                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)))
+    L = _lib.lib()
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(L.thz_czt_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+    ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
+    out = torch.empty((B, C, int(outW), int(outH)), dtype=torch.complex64, device=data.device)
+    with torch.cuda.device(data.device):
+        _lib.check(L.thz_czt_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
+                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                     ctypes.c_size_t(ws.numel()), _stream_handle()))
+    return out
