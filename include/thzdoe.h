@@ -20,6 +20,7 @@
  * Reference interfaces replaced (paths relative to the reference repo root):
  *   thz_asm_*        Props/ASM_Prop.py:17-378    ASM_prop.forward (+ autograd adjoint)
  *   thz_czt_*        Props/CZT_Prop.py:11-314    CZT_prop.forward / VCZT_prop
+ *   thz_rsc_*        Props/RSC_Prop.py:15-321    RSC_prop.forward / VRS_prop.forward
  *   thz_fft_*        utils/Helper_Functions.py:99-160 ft2/ift2 (centred ortho FFT)
  */
 #ifndef THZDOE_H_
@@ -101,6 +102,26 @@ typedef struct thz_czt_desc {
 
 int thz_czt_workspace_size(const thz_czt_desc* d, size_t* bytes);
 int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
+                    thz_stream_t stream);
+
+/*
+ * Rayleigh-Sommerfeld convolution, Props/RSC_Prop.py:170-215 (RSC_prop.forward), and its
+ * vectorial form VRS_prop.forward (:265-321, vectorial != 0: planes 0/1 of the input are
+ * Ex/Ey, Ez = (Ex x + Ey y)/r is formed in the kernel, output has 3 planes).
+ *   in  [B, C, H, W] -> out [Bo, C, Ph - H, Pw - W], Ph = H + 2 floor(H/2) (the reference's
+ *   ifft2(...)[..., H:, W:] window, :207), Bo = vectorial ? 3 : B.
+ * The spatial kernel grid uses dx on both axes (:83-84) and the spectrum is scaled by dx*dy.
+ */
+typedef struct thz_rsc_desc {
+  int B, C, H, W;
+  int vectorial;
+  float dx, dy;
+  float z;
+  const float* wavelengths; /* host [C] */
+} thz_rsc_desc;
+
+int thz_rsc_workspace_size(const thz_rsc_desc* d, size_t* bytes);
+int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
                     thz_stream_t stream);
 
 /*

@@ -1,0 +1,111 @@
+"""Rayleigh-Sommerfeld convolution, RSC_prop / VRS_prop -- drop-in for Props/RSC_Prop.py.
+
+Same constructor (``z_distance, device``; :17-45), ``z`` property (:47-57),
+``compute_padding`` (:60-77, padding scale 1), once-per-instance minimum-distance diagnostic
+(:89-127) and ``forward(field) -> ElectricField`` (:170-215, :265-321).  As in the
+reference, RSC_prop takes a single field (B == 1, :198-200) and the output window is
+ifft2(...)[..., H:, W:] (so an odd N returns N-1 samples, :207); VRS_prop forms Ez from the
+field's Ex/Ey planes and returns 3 planes.  One documented difference: where the reference's
+diagnostic crashes (z_min1 = 0 is an int without ``.detach``, :112-117) this mirror prints
+0.000 mm and continues.  The math runs in libthzdoe's gfx950 kernels (the spatial-kernel
+FFT and the convolution passes of thz_asm.hip).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+from quantizationawarethzdoe_amd import propagation as _prop
+
+mm = 1e-3
+
+
+def _f(v):
+    return float(v.detach().cpu()) if torch.is_tensor(v) else float(v)
+
+
+class RSC_prop(nn.Module):
+    _vectorial = False
+
+    def __init__(self, z_distance: float = 0.0, device: str = None) -> None:
+        super().__init__()
+        self.do_padding = True
+        self.DEFAULT_PADDING_SCALE = torch.tensor([1, 1])
+        self.device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+        self._z = torch.tensor(z_distance, device=self.device)
+        self._zh = _f(z_distance)
+        self.shape = None
+        self.check_Zc = True
+
+    @property
+    def z(self):
+        return self._z
+
+    @z.setter
+    def z(self, z) -> None:
+        if isinstance(z, torch.Tensor) and z.device != torch.device(self.device):
+            z = z.to(self.device)
+        self._z = z
+        self._zh = _f(z)
+
+    def compute_padding(self, H, W, return_size_of_padding=False):
+        """Props/RSC_Prop.py:60-77."""
+        ph, pw = (int(np.floor(H / 2)), int(np.floor(W / 2))) if self.do_padding else (0, 0)
+        if return_size_of_padding:
+            return ph, pw
+        return H + 2 * ph, W + 2 * pw
+
+    def check_RS_minimum_z(self, quality_factor=1, dx=None, dy=None, wavelength=None, Ph=None):
+        """Energy-conservation / sampling minimum distances, printed (Props/RSC_Prop.py:89-127)."""
+        f32 = np.float32
+        dx, dy, lam = f32(dx), f32(dy), f32(wavelength)
+        range_x, range_y = f32(self.shape[-2]) * dx, f32(self.shape[-1]) * dy
+        dr = np.sqrt(dx ** 2 + dy ** 2)
+        rmax = np.sqrt(range_x ** 2 + range_y ** 2)
+        factor = (((f32(quality_factor) * dr + rmax) ** 2 - lam ** 2 - rmax ** 2) / (f32(2) * lam)) ** 2 - rmax ** 2
+        z_min1 = np.sqrt(factor) if factor > 0 else f32(0)
+        print("Minimum propagation distance to satisfy energy conservation: {:.3f} mm".format(z_min1 / mm))
+        with np.errstate(invalid="ignore"):
+            z_min2 = f32(Ph) * dx ** 2 / lam * np.sqrt(f32(1) - (lam / (f32(2) * dx)) ** 2)
+        print("Minimum propagation distance to satisfy sampling for FT: {:.3f} mm".format(z_min2 / mm))
+        if self._zh > min(z_min1, z_min2):
+            print("The simulation will be accurate !")
+        else:
+            print("The propagation distance should be larger than minimum propagation distance to keep "
+                  "simulation accurate!")
+
+    def forward(self, field: ElectricField) -> ElectricField:
+        data = field.data
+        B, C, H, W = self.shape = data.shape
+        if not self._vectorial and B != 1:
+            raise RuntimeError(f"RSC_prop convolves a single field (B == 1) as the reference does "
+                               f"(Props/RSC_Prop.py:198-200); got B={B}")
+        sp = field.spacing_host
+        wl = field.wavelengths_host
+        if self.check_Zc:
+            self.check_RS_minimum_z(1, sp[0], sp[1], min(wl), Ph=H + 2 * (H // 2))
+            self.check_Zc = False
+        cdt = data.dtype
+        x = data if cdt == torch.complex64 else data.to(torch.complex64)
+        out = _RscFunction.apply(x, tuple(wl), tuple(sp), self._zh, self._vectorial)
+        if cdt != torch.complex64:
+            out = out.to(cdt)
+        Eout = ElectricField(data=out, wavelengths=field.wavelengths, spacing=field.spacing, device=field.device)
+        return Eout._adopt_host(field)
+
+
+class VRS_prop(RSC_prop):
+    """Vectorial RS: Ez = (Ex x + Ey y) / r, then the scalar convolution per component (:218-321)."""
+    _vectorial = True
+
+
+class _RscFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, data, wavelengths, spacing, z, vectorial):
+        return _prop.rsc_apply(data, wavelengths, spacing, z, vectorial)
+
+    @staticmethod
+    def backward(ctx, g):
+        raise NotImplementedError("RSC_prop backward is not implemented on the MI355X path yet")

@@ -28,6 +28,7 @@ EXPORTED = [
     "thz_version", "thz_last_error",
     "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band",
     "thz_czt_workspace_size", "thz_czt_forward",
+    "thz_rsc_workspace_size", "thz_rsc_forward",
     "thz_fft_rows",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
@@ -61,6 +62,14 @@ class CztDesc(ctypes.Structure):
     ]
 
 
+class RscDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("vectorial", ctypes.c_int), ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("z", ctypes.c_float),
+        ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
 _lib = None
 _lock = threading.Lock()
 
@@ -73,6 +82,8 @@ def _declare(lib):
     lib.thz_asm_forward.argtypes = [ctypes.POINTER(AsmDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_asm_band.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]
     lib.thz_fft_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+    lib.thz_rsc_workspace_size.argtypes = [ctypes.POINTER(RscDesc), ctypes.POINTER(c_size_t)]
+    lib.thz_rsc_forward.argtypes = [ctypes.POINTER(RscDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_czt_workspace_size.argtypes = [ctypes.POINTER(CztDesc), ctypes.POINTER(c_size_t)]
     lib.thz_czt_forward.argtypes = [ctypes.POINTER(CztDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]

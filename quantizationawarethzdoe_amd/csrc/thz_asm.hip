@@ -41,6 +41,9 @@ struct AsmArgs {
   int nz, zoff;                   // z-planes in this chunk, offset into zv
   int bl, adjoint;
   float dx, dy, scale;
+  const float2* tft;  // RSC: column-major transfer-function table [C][ncols][Ph] (nullptr: analytic ASM)
+  int vec;            // VRS: plane b == 2 is Ez = (Ex x + Ey y) / r computed in the row pass
+  float zr;           // VRS: z of the Ez grid
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
@@ -138,6 +141,13 @@ __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
 // ---------------------------------------------------------------------------------------------
 // K1: row FFT of the zero-padded input rows -> band columns, column-major T[bc][c][h]
 // ---------------------------------------------------------------------------------------------
+#pragma clang fp contract(off)
+__device__ __forceinline__ float2 vrs_ez(float2 ex, float2 ey, float x, float y, float z) {
+  const float r = sqrtf(x * x + y * y + z * z);
+  return make_float2((ex.x * x) / r + (ey.x * y) / r, (ex.y * x) / r + (ey.y * y) / r);
+}
+#pragma clang fp contract(on)
+
 template <int PN>
 __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
                                                     FftPlan pw, AsmArgs a) {
@@ -147,10 +157,20 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
   const int tid = threadIdx.x, nt = blockDim.x;
   const float2* src = in + ((size_t)bc * a.Hin + h) * a.Win;
   float2* dst = T + (size_t)bc * a.ncb * CB * a.Hin;
+  // VRS (Props/RSC_Prop.py:294-303): plane b = 2 is Ez = Ex x / r + Ey y / r on the unpadded
+  // grid linspace(-N dx/2, N dx/2, N) (dx on both axes, :83-84)
+  const bool ez = a.vec && bc / a.C == 2;
+  const float2* sx = in + ((size_t)(bc % a.C) * a.Hin + h) * a.Win;
+  const float2* sy = in + ((size_t)(a.C + bc % a.C) * a.Hin + h) * a.Win;
+  const float xh = ez ? lin(-(float)a.Hin * a.dx / 2.0f, (float)a.Hin * a.dx / 2.0f, a.Hin, h) : 0.f;
+  auto fetch = [&](int s) {
+    if (!ez) return src[s];
+    return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
+  };
   if constexpr (PN > 0) {
     auto ld = [&](int, int, int idx) {
       const int s = idx - a.in_c0;
-      return (s >= 0 && s < a.Win) ? src[s] : make_float2(0.f, 0.f);
+      return (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int c = band_col(j, PN, a.J, a.ncols);
@@ -160,7 +180,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
-      lds[padx(j)] = (s >= 0 && s < a.Win) ? src[s] : make_float2(0.f, 0.f);
+      lds[padx(j)] = (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
     }
     __syncthreads();
     fft_lds<false>(lds, pw, tid, nt);
@@ -202,6 +222,19 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
     fft_pow2_io<false, PN, TT, false, false, false>(lds, ph.tw, tid, ld0, sv0);
+    if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
+      const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
+      int tz = threadIdx.x;
+      asm volatile("" : "+v"(tz));
+      auto ld1 = [&](int m, int r, int idx) { return cmul(sp[m][r], tcol[idx]); };
+      float2* dst = U + (size_t)bc * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
+      auto sv1 = [&](int, int, int j, float2 v) {
+        const int r = j - a.out_r0;
+        if (r >= 0 && r < a.Hout) dst[(size_t)r * CB] = cscale(v, a.scale);
+      };
+      fft_pow2_io<true, PN, TT, true, false, false>(lds, ph.tw, tz, ld1, sv1);
+      return;
+    }
     // The evanescent and band-limit masks are monotone in |m_x| (every fp32 operation of
     // Props/ASM_Prop.py:245-306 is monotone), so for each z the kept rows of this column are
     // exactly |m_x| <= M_z.  One lane per z finds M_z by bisection with the exact
@@ -272,6 +305,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       const int i = tid + m * nt;
       sp[m] = i < Ph ? lds[padx(i)] : make_float2(0.f, 0.f);
     }
+    const float2* tcol = a.tft ? a.tft + ((size_t)(bc % a.C) * a.ncols + c) * Ph : nullptr;
     for (int zz = 0; zz < a.nz; ++zz) {
       const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
       int tm = threadIdx.x;
@@ -280,7 +314,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
 #pragma unroll
       for (int m = 0; m < FFT_MAXV; ++m) {
         const int i = tm + m * nt;
-        if (i < Ph) lds[padx(i)] = cmul(sp[m], tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky));
+        if (i < Ph)
+          lds[padx(i)] = cmul(sp[m], tcol ? tcol[i] : tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky));
       }
       __syncthreads();
       fft_lds<true>(lds, ph, tm, nt);
@@ -320,6 +355,65 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
     __syncthreads();
     fft_lds<true>(lds, pw, tid, nt);
     for (int w = tid; w < a.Wout; w += nt) dst[w] = lds[padx(a.out_c0 + w)];
+  }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// RSC (Props/RSC_Prop.py:129-215): transfer function = FFT2 of the spatial RS kernel on the
+// P = N + 2 floor(N/2) grid, stored column-major [C][Pw][Ph] for the column pass.
+// ---------------------------------------------------------------------------------------------
+struct RscKArgs {
+  int C, Ph, Pw, ncbK;
+  float dx, z;
+  float lam[THZ_MAX_WAVELENGTHS];
+};
+
+template <int PN>
+__global__ void __launch_bounds__(1024) rsc_k_rows(float2* __restrict__ TK, FftPlan pw, RscKArgs k) {
+  extern __shared__ float2 lds[];
+  const int row = blockIdx.x;
+  const int c = row / k.Ph, i = row - c * k.Ph;
+  const float lam = k.lam[c];
+  const float kk = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, k.z);
+  // grid x = linspace(-P dx/2, P dx/2, P) on both axes with dx (:83-84)
+  const float xi = lin(-(float)k.Ph * k.dx / 2.0f, (float)k.Ph * k.dx / 2.0f, k.Ph, i);
+  const float ylo = -(float)k.Pw * k.dx / 2.0f, yhi = (float)k.Pw * k.dx / 2.0f;
+  float2* dst = TK + (size_t)c * k.ncbK * CB * k.Ph;
+  auto load = [&](int j) { return rs_kernel(xi, lin(ylo, yhi, k.Pw, j), k.z, kk, rph); };
+  auto store = [&](int j, float2 v) { dst[blk(band_col(j, k.Pw, k.Pw / 2, k.Pw), i, k.Ph)] = v; };
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if constexpr (PN > 0) {
+    auto ld = [&](int, int, int j) { return load(j); };
+    auto sv = [&](int, int, int j, float2 v) { store(j, v); };
+    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
+  } else {
+    for (int j = tid; j < k.Pw; j += nt) lds[padx(j)] = load(j);
+    __syncthreads();
+    fft_lds<false>(lds, pw, tid, nt);
+    for (int j = tid; j < k.Pw; j += nt) store(j, lds[padx(j)]);
+  }
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) rsc_k_cols(const float2* __restrict__ TK, float2* __restrict__ KF,
+                                                  FftPlan ph, RscKArgs k) {
+  extern __shared__ float2 lds[];
+  const int id = xcd_chunk(blockIdx.x, gridDim.x);
+  const int c = id / k.Pw, cc = id - c * k.Pw;
+  const float2* col = TK + (size_t)c * k.ncbK * CB * k.Ph + blk(cc, 0, k.Ph);
+  float2* dst = KF + ((size_t)c * k.Pw + cc) * k.Ph;
+  const int tid = threadIdx.x, nt = blockDim.x;
+  if constexpr (PN > 0) {
+    auto ld = [&](int, int, int i) { return col[(size_t)i * CB]; };
+    auto sv = [&](int, int, int i, float2 v) { dst[i] = v; };
+    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, ph.tw, tid, ld, sv);
+  } else {
+    for (int i = tid; i < k.Ph; i += nt) lds[padx(i)] = col[(size_t)i * CB];
+    __syncthreads();
+    fft_lds<false>(lds, ph, tid, nt);
+    for (int i = tid; i < k.Ph; i += nt) dst[i] = lds[padx(i)];
   }
 }
 
@@ -457,6 +551,8 @@ static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_cols<PN>);
   ks.push_back((const void*)asm_rows_inv<PN>);
   ks.push_back((const void*)fft_rows_kernel<PN>);
+  ks.push_back((const void*)rsc_k_rows<PN>);
+  ks.push_back((const void*)rsc_k_cols<PN>);
 }
 
 // Workgroups above 64 KiB of dynamic LDS must opt in once per kernel.
@@ -487,6 +583,40 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 static size_t ws_bytes(const AsmGeom& g) {
   return align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)) +
          align256((size_t)g.zc * g.BC * g.ncb * CB * g.Hout * sizeof(float2));
+}
+
+// K1 once, then (K2, K3) per z-chunk, on a prepared argument block.
+static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
+                        hipStream_t s, FftPlan pw, FftPlan ph) {
+  int e;
+  if ((e = ensure_lds_attr())) return e;
+  const int tw = threads_for(g.Pw), th = threads_for(g.Ph);
+  {
+    KernelTimer kt("asm_rows_fwd", s);
+    THZ_POW2_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), dim3(tw), fft_lds_bytes(g.Pw), s, (const float2*)in,
+                    T, pw, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  for (int z0 = 0; z0 < Z; z0 += g.zc) {
+    a.zoff = z0;
+    a.nz = std::min(g.zc, Z - z0);
+    {
+      KernelTimer kt("asm_cols", s);
+      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols * g.BC), dim3(th), fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z, s,
+                      (const float2*)T, U, ph, a);
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+    {
+      KernelTimer kt("asm_rows_inv", s);
+      THZ_POW2_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), dim3(tw), fft_lds_bytes(g.Pw), s,
+                      (const float2*)U, (float2*)out, pw, a);
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+  }
+  return THZ_OK;
 }
 
 }  // namespace thz
@@ -552,38 +682,9 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
   for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
   for (int zi = 0; zi < d->Z; ++zi) a.zv[zi] = d->z[zi];
 
-  hipStream_t s = (hipStream_t)stream;
-  if ((e = ensure_lds_attr())) return e;
   float2* T = (float2*)workspace;
   float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
-  const int tw = threads_for(g.Pw), th = threads_for(g.Ph);
-
-  {
-    KernelTimer kt("asm_rows_fwd", s);
-    THZ_POW2_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), dim3(tw), fft_lds_bytes(g.Pw), s, (const float2*)in,
-                    T, pw, a);
-    THZ_LAUNCH_CHECK();
-    kt.stop();
-  }
-  for (int z0 = 0; z0 < d->Z; z0 += g.zc) {
-    a.zoff = z0;
-    a.nz = std::min(g.zc, d->Z - z0);
-    {
-      KernelTimer kt("asm_cols", s);
-      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols * g.BC), dim3(th), fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z, s, (const float2*)T, U,
-                      ph, a);
-      THZ_LAUNCH_CHECK();
-      kt.stop();
-    }
-    {
-      KernelTimer kt("asm_rows_inv", s);
-      THZ_POW2_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), dim3(tw), fft_lds_bytes(g.Pw), s,
-                      (const float2*)U, (float2*)out, pw, a);
-      THZ_LAUNCH_CHECK();
-      kt.stop();
-    }
-  }
-  return THZ_OK;
+  return run_pipeline(a, g, d->Z, in, out, T, U, (hipStream_t)stream, pw, ph);
 }
 
 extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream) {
@@ -596,4 +697,112 @@ extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inve
                   (const float2*)in, (float2*)out, p, inverse);
   THZ_LAUNCH_CHECK();
   return THZ_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// RSC / VRS C-ABI
+// ---------------------------------------------------------------------------------------------
+namespace thz {
+
+struct RscPlan {
+  AsmGeom g;
+  RscKArgs k;
+  size_t tk, kf, t, u;  // byte sizes
+};
+
+static int rsc_plan(const thz_rsc_desc* d, RscPlan* p) {
+  if (!d) return fail(THZ_E_ARG, "null descriptor");
+  if (d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1) return fail(THZ_E_ARG, "bad RSC shape");
+  if (d->vectorial && d->B < 2) return fail(THZ_E_ARG, "vectorial RSC needs Ex, Ey planes (B >= 2)");
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  if (!d->wavelengths) return fail(THZ_E_ARG, "null wavelengths");
+  AsmGeom& g = p->g;
+  g.Ph = d->H + 2 * (d->H / 2);
+  g.Pw = d->W + 2 * (d->W / 2);
+  if (g.Ph > FFT_MAX_N || g.Pw > FFT_MAX_N) return fail(THZ_E_UNSUPPORTED, "RSC grid %dx%d too large", g.Ph, g.Pw);
+  g.BC = (d->vectorial ? 3 : d->B) * d->C;
+  g.Hin = d->H;
+  g.Win = d->W;
+  g.Hout = g.Ph - d->H;  // ifft2(...)[..., H:, W:] (:207)
+  g.Wout = g.Pw - d->W;
+  g.ncols = g.Pw;
+  g.J = g.Pw / 2;
+  g.ncb = (g.ncols + CB - 1) / CB;
+  g.zc = 1;
+  RscKArgs& k = p->k;
+  k.C = d->C;
+  k.Ph = g.Ph;
+  k.Pw = g.Pw;
+  k.ncbK = g.ncb;
+  k.dx = d->dx;
+  k.z = d->z;
+  for (int c = 0; c < d->C; ++c) k.lam[c] = d->wavelengths[c];
+  p->tk = align256((size_t)d->C * k.ncbK * CB * g.Ph * sizeof(float2));
+  p->kf = align256((size_t)d->C * g.Pw * g.Ph * sizeof(float2));
+  p->t = align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2));
+  p->u = align256((size_t)g.BC * g.ncb * CB * g.Hout * sizeof(float2));
+  return THZ_OK;
+}
+
+}  // namespace thz
+
+extern "C" int thz_rsc_workspace_size(const thz_rsc_desc* d, size_t* bytes) {
+  RscPlan p;
+  int e = rsc_plan(d, &p);
+  if (e) return e;
+  if (!bytes) return fail(THZ_E_ARG, "null bytes");
+  *bytes = p.tk + p.kf + p.t + p.u;
+  return THZ_OK;
+}
+
+extern "C" int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out, void* workspace,
+                               size_t workspace_bytes, thz_stream_t stream) {
+  RscPlan p;
+  int e = rsc_plan(d, &p);
+  if (e) return e;
+  if (!in || !out) return fail(THZ_E_ARG, "null data pointer");
+  if (!workspace || workspace_bytes < p.tk + p.kf + p.t + p.u)
+    return fail(THZ_E_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, p.tk + p.kf + p.t + p.u);
+  if ((e = ensure_lds_attr())) return e;
+  const AsmGeom& g = p.g;
+  FftPlan pw, ph;
+  if ((e = get_plan(g.Pw, &pw))) return e;
+  if ((e = get_plan(g.Ph, &ph))) return e;
+  hipStream_t s = (hipStream_t)stream;
+  char* w = (char*)workspace;
+  float2* TK = (float2*)w;
+  float2* KF = (float2*)(w + p.tk);
+  float2* T = (float2*)(w + p.tk + p.kf);
+  float2* U = (float2*)(w + p.tk + p.kf + p.t);
+  {
+    KernelTimer kt("rsc_kernel_fft", s);
+    THZ_POW2_SWITCH(g.Pw, rsc_k_rows, dim3(d->C * g.Ph), dim3(threads_for(g.Pw)), fft_lds_bytes(g.Pw), s, TK, pw,
+                    p.k);
+    THZ_LAUNCH_CHECK();
+    THZ_POW2_SWITCH(g.Ph, rsc_k_cols, dim3(d->C * g.Pw), dim3(threads_for(g.Ph)), fft_lds_bytes(g.Ph), s,
+                    (const float2*)TK, KF, ph, p.k);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  AsmArgs a{};
+  a.BC = g.BC;
+  a.C = d->C;
+  a.Ph = g.Ph;
+  a.Pw = g.Pw;
+  a.in_r0 = 0; a.in_c0 = 0; a.Hin = d->H; a.Win = d->W;         // U[..., :H, :W] = field (:198-200)
+  a.out_r0 = d->H; a.out_c0 = d->W; a.Hout = g.Hout; a.Wout = g.Wout;
+  a.ncols = g.ncols;
+  a.ncb = g.ncb;
+  a.J = g.J;
+  a.bl = THZ_BANDLIMIT_NONE;
+  a.dx = d->dx;
+  a.dy = d->dy;
+  a.scale = (float)((double)d->dx * (double)d->dy / ((double)g.Ph * (double)g.Pw));
+  a.tft = KF;
+  a.vec = d->vectorial;
+  a.zr = d->z;
+  a.lam[0] = d->wavelengths[0];
+  for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
+  a.zv[0] = d->z;
+  return run_pipeline(a, g, 1, in, out, T, U, s, pw, ph);
 }

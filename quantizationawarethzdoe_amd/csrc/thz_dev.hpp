@@ -72,4 +72,46 @@ __device__ __forceinline__ float2 cis_d(double ph) {
 
 __device__ __forceinline__ int freq_index(int i, int n) { return i < n - n / 2 ? i : i - n; }
 
+// RS kernel exp(ikr) z/(2 pi r^2) (1/r - ik) (Props/CZT_Prop.py:44-57).  The amplitude is
+// fp32 in the reference's operation order; the phase k r (thousands of radians) is formed as
+// (k|z| mod 2 pi, from double) + k rho^2 / (r + |z|) -- the exact identity r - |z| =
+// rho^2/(r + |z|) keeps the fp32 part small, so the phase error drops from ~2e-4 rad (fp32
+// k*r, which the reference pays and which costs it ~4e-3 rel-L2 on the test_czt.py case)
+// to ~3e-5 rad.
+struct RsPhase {
+  float kzmod;  // (k |z|) mod 2 pi, k = 2 pi / lambda, evaluated in double
+  float k;
+};
+__device__ __forceinline__ RsPhase rs_phase(float lam, float z) {
+  const double k = 6.283185307179586476925 / (double)lam;
+  double kz = k * fabs((double)z);
+  kz -= 6.283185307179586476925 * floor(kz / 6.283185307179586476925);
+  RsPhase p;
+  p.kzmod = (float)kz;
+  p.k = (float)k;
+  return p;
+}
+
+#pragma clang fp contract(off)
+__device__ __forceinline__ float2 rs_kernel(float x, float y, float z, float k, const RsPhase& ph) {
+  const float rho2 = x * x + y * y;
+  const float r = sqrtf(rho2 + z * z);
+  const float f = 0.15915494309189535f * z / (r * r);
+  const float fr = f * (1.0f / r), fi = -(f * k);
+  float sn, cs;
+  sincos_rad(ph.kzmod + ph.k * (rho2 / (r + fabsf(z))), &sn, &cs);
+  return make_float2(cs * fr - sn * fi, cs * fi + sn * fr);
+}
+
+// torch.linspace(start, end, n)[i] in fp32 (symmetric two-sided form of ATen's CPU kernel)
+__device__ __forceinline__ float lin(float start, float end, int n, int i) {
+  if (n == 1) return start;
+  const float step = (end - start) / (float)(n - 1);
+  const int half = n / 2;
+  return i < half ? start + step * (float)i : end - step * (float)(n - 1 - i);
+}
+#pragma clang fp contract(on)
+
+
+
 }  // namespace thz
