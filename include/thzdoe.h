@@ -21,6 +21,8 @@
  *   thz_asm_*        Props/ASM_Prop.py:17-378    ASM_prop.forward (+ autograd adjoint)
  *   thz_czt_*        Props/CZT_Prop.py:11-314    CZT_prop.forward / VCZT_prop
  *   thz_rsc_*        Props/RSC_Prop.py:15-321    RSC_prop.forward / VRS_prop.forward
+ *   thz_doe_*        Components/QuantizedDOE.py:44-126  DOELayer.modulate (+ backward)
+ *   thz_quant_*      Components/QuantizedDOE.py:181-1388 quantized height maps (+ backward)
  *   thz_fft_*        utils/Helper_Functions.py:99-160 ft2/ift2 (centred ortho FFT)
  */
 #ifndef THZDOE_H_
@@ -123,6 +125,72 @@ typedef struct thz_rsc_desc {
 int thz_rsc_workspace_size(const thz_rsc_desc* d, size_t* bytes);
 int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
                     thz_stream_t stream);
+
+/*
+ * DOE modulation, DOELayer.modulate (Components/QuantizedDOE.py:92-126):
+ *   h' = height + (noise - 0.5) * 2 * tolerance   (noise = the rand_like draw, NULL = no noise, :82-87)
+ *   h_full = nearest-upsample(h') to [H, W]        (:102-107)
+ *   out[b,c] = field[b,c] * exp(-k_c/2 (h+b) tand sqrt(eps)) exp(-i k_c (h+b)(sqrt(eps)-1))  (:47-79)
+ * field/out [B, C, H, W] complex64; height/noise [hs, ws] float32 (device).  height_full, if
+ * non-NULL, receives h_full [H, W].  Backward: grad_field = g conj(t) (NULL to skip) and
+ * grad_height [hs, ws] = sum_bc Re(g conj(field) conj(dt/dh)) (NULL to skip).
+ */
+typedef struct thz_doe_desc {
+  int B, C, H, W;
+  int hs, ws;                /* height-map size (upsampled to H, W if different) */
+  float tolerance, epsilon, tand;
+  const float* wavelengths;  /* host [C] */
+} thz_doe_desc;
+
+int thz_doe_modulate_forward(const thz_doe_desc* d, const void* field, const float* height, const float* noise,
+                             void* out, float* height_full, thz_stream_t stream);
+int thz_doe_modulate_backward(const thz_doe_desc* d, const void* grad_out, const void* field, const float* height,
+                              const float* noise, void* grad_field, float* grad_height, thz_stream_t stream);
+
+/*
+ * Height-map quantizers of the QAT layers (forward value + custom backward), one fused kernel
+ * each way.  weight: [hq, wq] (FP/STE/PSQ/SGV3) or [hq, wq, L] logits (NGS).  height_full:
+ * [2hq, 2wq] when mirror (num_unit set, _copy_quad_to_full :28-35) else [hq, wq].
+ * noise_exp: the Exp(1) draw F.gumbel_softmax consumes ([L, hq, wq] for SGV1 and for SGV3
+ * when iter_frac > 0.3, [hq, wq, L] for NGS); y_soft (same shape) is saved for the backward.
+ * SoftGumbelQuantizedDOELayerv2 (:608-635) is SGV3 with iter_frac passed as 0 or 1.
+ */
+#define THZ_Q_FP 0    /* FullPrecisionDOELayer            :286-292   */
+#define THZ_Q_STE 1   /* STEQuantizedDOELayer             :1239-1388 */
+#define THZ_Q_PSQ 2   /* PSQuantizedDOELayer              :1193-1223 */
+#define THZ_Q_SGV3 3  /* SoftGumbelQuantizedDOELayerv3    :794-860   */
+#define THZ_Q_NGS 4   /* NaiveGumbelQuantizedDOELayer     :1022-1041 */
+#define THZ_Q_SGV1 5  /* SoftGumbelQuantizedDOELayer      :411-456 (weight = phase) */
+#define THZ_MAX_LUT 16
+
+typedef struct thz_quant_desc {
+  int kind;
+  int hq, wq;
+  int mirror;
+  int L;
+  const float* lut;   /* host [L] */
+  float hmax;         /* height_constraint_max */
+  float clamp;        /* weight clamp: 8 (FP/STE/PSQ), 10 (SGV3) */
+  float tau;          /* temperature of the layer's schedule */
+  float iter_frac;    /* SGV3 schedule phase */
+  float c_s;          /* SGV3 score boost */
+  float s;            /* SGV3 steepness tau_max / tau */
+  float beta;         /* SGV3 blend (iter_frac - 0.3) / 0.5 */
+  float phase_scale;  /* SGV3 2 pi / lambda_min * (sqrt(eps) - 1), fp32 */
+} thz_quant_desc;
+
+int thz_quant_forward(const thz_quant_desc* d, const float* weight, const float* noise_exp, float* height_full,
+                      float* y_soft, thz_stream_t stream);
+int thz_quant_backward(const thz_quant_desc* d, const float* weight, const float* y_soft, const float* grad_full,
+                       float* grad_weight, thz_stream_t stream);
+
+/*
+ * Radial profile -> 2-D height map of the rotationally symmetric layers
+ * (Components/QuantizedDOE.py:1409-1433): quadrant pixel (x, y) takes profile[floor(r)] for
+ * r = sqrt(x^2 + y^2) < R - 1 (0 beyond), mirrored to 2R x 2R and centre-cropped to [H, W].
+ */
+int thz_radial_forward(const float* profile, int R, int H, int W, float* out, thz_stream_t stream);
+int thz_radial_backward(const float* grad_out, int R, int H, int W, float* grad_profile, thz_stream_t stream);
 
 /*
  * Batched 1-D FFT along the contiguous axis (the building block of ft2/ift2,

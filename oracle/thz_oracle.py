@@ -301,6 +301,102 @@ def ste_quantize(h, lut):
     return lut[idx]
 
 
+def fp_height(weight, hmax, clamp=8.0):
+    """h_max * sigmoid(clamp(w)) (QuantizedDOE.py:287, :823 with clamp 10)."""
+    return hmax * torch.sigmoid(torch.clamp(weight, min=-clamp, max=clamp))
+
+
+def gumbel_hard(logits, tau, expo, dim):
+    """F.gumbel_softmax(hard=True) with the Exp(1) draw injected: straight-through one-hot."""
+    y = torch.softmax((logits + (-torch.log(expo))) / tau, dim=dim)
+    idx = y.argmax(dim=dim, keepdim=True)
+    hard = torch.zeros_like(y).scatter_(dim, idx, 1.0)
+    return hard - y.detach() + y
+
+
+def psq_height(weight, hmax, L, tau):
+    """PSQuantizedDOELayer.preprocessed_height_map (QuantizedDOE.py:1193-1216), before mirroring."""
+    h = fp_height(weight, hmax, 8.0)
+    delta = (hmax - 0) / (L - 1)
+    xn = (h - 0) / delta - 0.5
+    levels = torch.arange(L - 1).unsqueeze(0).unsqueeze(2)
+    return 0 + delta * torch.sum(torch.sigmoid(tau * (xn.unsqueeze(1) - levels)), dim=1)
+
+
+def radial_map(profile, R, H, W):
+    """Rotationally symmetric expansion (QuantizedDOE.py:1412-1432): bins floor(r) < R-1."""
+    x, y = torch.meshgrid(torch.arange(0, R), torch.arange(0, R), indexing="ij")
+    r = torch.sqrt(x ** 2 + y ** 2)
+    quad = torch.where((r < 1.0) & (r >= 0.0), profile[0], 0)
+    for k in range(1, R - 1):
+        quad = quad + torch.where((r < float(k + 1)) & (r >= float(k)), profile[k], 0)
+    full = copy_quad_to_full(quad)
+    sx, sy = R - H // 2, R - W // 2
+    return full[sx:sx + H, sy:sy + W]
+
+
+def _scores(phase, plut, tau, c_s, tau_max):
+    return sgv3_score(phase, plut, tau_max / tau) * c_s * (tau_max / tau)
+
+
+def layer_height_map(cls, weight, lut, hmax, lam_min, eps, iter_frac, optim, num_unit, doe_size, expo=None):
+    """preprocessed_height_map of every QAT layer class (QuantizedDOE.py:286-1623), RNG injected.
+
+    ``weight`` is the layer's parameter as the reference shapes it; ``expo`` the Exp(1) draw.
+    """
+    L = len(lut)
+    n = torch.sqrt(torch.as_tensor(eps, dtype=torch.float32))
+    tmin, tmax = optim.get("tau_min"), optim.get("tau_max")
+    cos_tau = sgv3_tau(iter_frac, tmin, tmax) if iter_frac is not None else None
+    mirror = (lambda h: copy_quad_to_full(h)) if num_unit is not None else (lambda h: h)
+    rot = cls.startswith("RotationallySymmetric")
+    R = int(doe_size[0] * torch.sqrt(torch.tensor(2)) / 2)
+    finish = (lambda p: radial_map(p.reshape(-1), R, doe_size[0], doe_size[1])) if rot else None
+    if cls in ("FullPrecisionDOELayer", "RotationallySymmetricFullPrecisionDOELayer"):
+        h = fp_height(weight, hmax, 8.0)
+        return finish(h) if rot else mirror(h.reshape(h.shape[-2:]))
+    if cls in ("STEQuantizedDOELayer", "RotationallySymmetricSTEQuantizedDOELayer"):
+        h = fp_height(weight, hmax, 8.0)
+        h = h if rot else mirror(h.reshape(h.shape[-2:]))
+        q = h + (ste_quantize(h, lut) - h).detach()  # identity gradient
+        return finish(q) if rot else q
+    if cls in ("PSQuantizedDOELayer", "RotationallySymmetricPSQuantizedQuantizedDOELayer"):
+        tau = tmin + (tmax - tmin) * iter_frac
+        h = psq_height(weight, hmax, L, tau)
+        return finish(h) if rot else mirror(h)
+    if cls in ("NaiveGumbelQuantizedDOELayer", "RotationallySymmetricNaiveGumbelQuantizedDOELayer"):
+        oh = gumbel_hard(weight, cos_tau if cos_tau is not None else 1, expo, -1)
+        h = (lut[None, None, :] * oh).sum(dim=-1)
+        return finish(h) if rot else mirror(h)
+    if cls == "SoftGumbelQuantizedDOELayer":
+        oh = gumbel_hard(_scores(weight, height_to_phase(lut, lam_min, n), cos_tau, optim["c_s"], tmax),
+                         cos_tau, expo, 1)
+        h = (lut.reshape(1, L, 1, 1) * oh).sum(1, keepdim=True)
+        if num_unit is not None:
+            raise NotImplementedError("v1 with num_unit tiles by the 4-D shape (reference quirk)")
+        return h[0, 0]
+    if cls in ("SoftGumbelQuantizedDOELayerv2", "SoftGumbelQuantizedDOELayerv3",
+               "RotationallySymmetricScoreGumbelSoftQuantizedDOELayer"):
+        h = fp_height(weight, hmax, 10.0)
+        if weight.dim() == 2:
+            h = h[None, None]
+        v2 = cls.endswith("v2")
+        quant = iter_frac > 0.5 if v2 else iter_frac > 0.3
+        if quant:
+            oh = gumbel_hard(_scores(height_to_phase(h, lam_min, n), height_to_phase(lut, lam_min, n), cos_tau,
+                                     optim["c_s"], tmax), cos_tau, expo, 1)
+            q = (lut.reshape(1, L, 1, 1) * oh).sum(1, keepdim=True)
+            if not v2 and iter_frac <= 0.8:
+                beta = iter_frac if rot else (iter_frac - 0.3) / (0.8 - 0.3)
+                h = (1 - beta) * h + beta * q
+            else:
+                h = q
+        if rot:
+            return finish(h)
+        return mirror(h[0, 0]) if not v2 else h[0, 0]
+    raise ValueError(f"unknown layer class {cls}")
+
+
 def normalize(x):
     """Per-batch divide by max (utils/Helper_Functions.py:185-193), out of place."""
     B = x.shape[0]

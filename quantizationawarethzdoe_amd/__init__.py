@@ -13,8 +13,21 @@ __version__ = "0.1.0"
 _ALIASES = ("DataType", "Props", "Components", "LightSource", "utils")
 
 
+_MODULES = ("DataType.ElectricField", "Props.ASM_Prop", "Props.CZT_Prop", "Props.RSC_Prop",
+            "Components.QuantizedDOE", "utils.units", "utils.Visualization_Helper")
+
+
 def install_reference_aliases():
-    """Make ``from Props.ASM_Prop import ASM_prop`` (the reference's import paths) resolve here."""
+    """Make ``from Props.ASM_Prop import ASM_prop`` (the reference's import paths) resolve here.
+
+    Submodules are imported eagerly so every alias names the same module object (one
+    ``ElectricField`` class whichever path a caller imports it by).
+    """
+    for sub in _MODULES:
+        try:
+            importlib.import_module(f"{__name__}.{sub}")
+        except ModuleNotFoundError:
+            pass
     for name in _ALIASES:
         mod = importlib.import_module(f"{__name__}.{name}")
         sys.modules[name] = mod

@@ -29,6 +29,8 @@ EXPORTED = [
     "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band",
     "thz_czt_workspace_size", "thz_czt_forward",
     "thz_rsc_workspace_size", "thz_rsc_forward",
+    "thz_doe_modulate_forward", "thz_doe_modulate_backward", "thz_quant_forward", "thz_quant_backward",
+    "thz_radial_forward", "thz_radial_backward",
     "thz_fft_rows",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
@@ -70,6 +72,28 @@ class RscDesc(ctypes.Structure):
     ]
 
 
+class DoeDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("hs", ctypes.c_int), ("ws", ctypes.c_int),
+        ("tolerance", ctypes.c_float), ("epsilon", ctypes.c_float), ("tand", ctypes.c_float),
+        ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+class QuantDesc(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int), ("hq", ctypes.c_int), ("wq", ctypes.c_int), ("mirror", ctypes.c_int),
+        ("L", ctypes.c_int), ("lut", ctypes.POINTER(ctypes.c_float)),
+        ("hmax", ctypes.c_float), ("clamp", ctypes.c_float), ("tau", ctypes.c_float),
+        ("iter_frac", ctypes.c_float), ("c_s", ctypes.c_float), ("s", ctypes.c_float),
+        ("beta", ctypes.c_float), ("phase_scale", ctypes.c_float),
+    ]
+
+
+Q_FP, Q_STE, Q_PSQ, Q_SGV3, Q_NGS, Q_SGV1 = 0, 1, 2, 3, 4, 5
+THZ_MAX_LUT = 16
+
 _lib = None
 _lock = threading.Lock()
 
@@ -84,6 +108,14 @@ def _declare(lib):
     lib.thz_fft_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
     lib.thz_rsc_workspace_size.argtypes = [ctypes.POINTER(RscDesc), ctypes.POINTER(c_size_t)]
     lib.thz_rsc_forward.argtypes = [ctypes.POINTER(RscDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.thz_doe_modulate_forward.argtypes = [ctypes.POINTER(DoeDesc), c_void_p, c_void_p, c_void_p, c_void_p,
+                                             c_void_p, c_void_p]
+    lib.thz_doe_modulate_backward.argtypes = [ctypes.POINTER(DoeDesc), c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p, c_void_p, c_void_p]
+    lib.thz_quant_forward.argtypes = [ctypes.POINTER(QuantDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.thz_quant_backward.argtypes = [ctypes.POINTER(QuantDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.thz_radial_forward.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]
+    lib.thz_radial_backward.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]
     lib.thz_czt_workspace_size.argtypes = [ctypes.POINTER(CztDesc), ctypes.POINTER(c_size_t)]
     lib.thz_czt_forward.argtypes = [ctypes.POINTER(CztDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]

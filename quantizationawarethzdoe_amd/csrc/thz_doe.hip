@@ -1,0 +1,491 @@
+// Quantization-aware DOE layers (Components/QuantizedDOE.py) for gfx950.
+//
+//  * modulate (DOELayer.modulate, :92-126): height noise (:82-87), nearest upsampling
+//    (:102-107), transmission t_c(h) = exp(-k/2 (h+b) tand sqrt(eps)) exp(-i k (h+b)(sqrt(eps)-1))
+//    (:47-79) and field * t, fused in one pass over the field; its backward in one more
+//    (grad_field = g conj(t); grad_h = sum_bc Re(g conj(f) conj(t gamma)), scattered to the
+//    source pixel of the nearest upsampling).
+//  * height-map quantizers, one thread per parameter pixel, forward and backward fused
+//    (every op of the reference chain in one kernel, the full mirrored map written directly):
+//      FP    FullPrecisionDOELayer      :286-292   h = hmax sigmoid(clamp(w, +-8))
+//      STE   STEQuantizedDOELayer       :1239-1388 nearest LUT level, identity gradient
+//      PSQ   PSQuantizedDOELayer        :1193-1223 sum of L-1 tempered sigmoids
+//      SGV3  SoftGumbelQuantizedDOELayerv3 :794-860 phase-score soft Gumbel (the paper's method)
+//      NGS   NaiveGumbelQuantizedDOELayer  :1022-1041 Gumbel-softmax over [h, w, L] logits
+//      SGV1  SoftGumbelQuantizedDOELayer   :411-456  phase-score soft Gumbel on a raw phase weight
+//    (SoftGumbelQuantizedDOELayerv2, :608-635, is SGV3 with its own threshold: the host passes the
+//    mode as iter_frac 0 or 1.)
+//    The Gumbel noise is injected (Exp(1) draws, -log(E) = Gumbel), so a caller can replay the
+//    reference's RNG stream exactly (tests) or draw it from any generator (training).
+#include <algorithm>
+#include <cmath>
+
+#include "thz_common.hpp"
+#include "thz_dev.hpp"
+
+// every fp32 operation in this file rounds as the reference's separate torch ops do
+#pragma clang fp contract(off)
+
+namespace thz {
+
+constexpr float BASE_PLANE = 2e-3f;  // BASE_PLANE_THICKNESS (:23)
+
+struct ModArgs {
+  int B, C, H, W, hs, ws;
+  int has_noise;
+  float tol, eps, tand;
+  float lam[THZ_MAX_WAVELENGTHS];
+};
+
+#pragma clang fp contract(off)
+// nearest source index of torch.nn.functional.interpolate(mode='nearest'), fp32 scale
+__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
+  if (in == out) return dst;
+  const float scale = (float)in / (float)out;
+  return min((int)floorf((float)dst * scale), in - 1);
+}
+
+// noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85)
+__device__ __forceinline__ float noisy_h(const float* h, const float* u, int idx, const ModArgs& a) {
+  float v = h[idx];
+  if (a.has_noise) v = v + ((u[idx] - 0.5f) * 2.0f) * a.tol;
+  return v;
+}
+
+// t_c(h) and gamma_c = dt/dh / t (:73-77)
+__device__ __forceinline__ float2 transmission(float hv, float lam, const ModArgs& a, float2* gamma) {
+  const float k = 6.283185307179586f / lam;
+  const float hb = hv + BASE_PLANE;
+  const float se = sqrtf(a.eps);
+  const float ga = ((-0.5f * k) * a.tand) * se;  // d(log loss)/dh
+  const float loss = expf(((-0.5f * k) * hb * a.tand) * se);
+  const float gb = -k * (se - 1.0f);             // d(phase)/dh
+  const float ph = (-k * hb) * (se - 1.0f);
+  float sn, cs;
+  sincos_rad(ph, &sn, &cs);
+  if (gamma) *gamma = make_float2(ga, gb);
+  return make_float2(loss * cs, loss * sn);
+}
+
+__global__ void doe_modulate_fwd(const float2* __restrict__ f, const float* __restrict__ h,
+                                 const float* __restrict__ u, float2* __restrict__ out, float* __restrict__ hfull,
+                                 ModArgs a) {
+  const int HW = a.H * a.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  const int y = p / a.W, x = p - y * a.W;
+  const int src = nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W);
+  const float hv = noisy_h(h, u, src, a);
+  if (hfull) hfull[p] = hv;
+  for (int c = 0; c < a.C; ++c) {
+    const float2 t = transmission(hv, a.lam[c], a, nullptr);
+    for (int b = 0; b < a.B; ++b) {
+      const size_t i = ((size_t)b * a.C + c) * HW + p;
+      out[i] = cmul(f[i], t);
+    }
+  }
+}
+
+__global__ void doe_modulate_bwd(const float2* __restrict__ g, const float2* __restrict__ f,
+                                 const float* __restrict__ h, const float* __restrict__ u,
+                                 float2* __restrict__ gf, float* __restrict__ gh, ModArgs a) {
+  const int HW = a.H * a.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  const int y = p / a.W, x = p - y * a.W;
+  const int src = nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W);
+  const float hv = noisy_h(h, u, src, a);
+  float acc = 0.f;
+  for (int c = 0; c < a.C; ++c) {
+    float2 gam;
+    const float2 t = transmission(hv, a.lam[c], a, &gam);
+    float2 gt = make_float2(0.f, 0.f);  // sum_b g conj(f)
+    for (int b = 0; b < a.B; ++b) {
+      const size_t i = ((size_t)b * a.C + c) * HW + p;
+      const float2 gv = g[i];
+      if (gf) gf[i] = make_float2(gv.x * t.x + gv.y * t.y, gv.y * t.x - gv.x * t.y);
+      if (gh) {
+        const float2 fv = f[i];
+        gt.x += gv.x * fv.x + gv.y * fv.y;
+        gt.y += gv.y * fv.x - gv.x * fv.y;
+      }
+    }
+    if (gh) {
+      const float2 dt = cmul(t, gam);  // dt/dh
+      acc += gt.x * dt.x + gt.y * dt.y;  // Re(gt conj(dt))
+    }
+  }
+  if (gh) {
+    if (a.hs == a.H && a.ws == a.W) gh[src] = acc;
+    else atomicAdd(gh + src, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// quantizers
+// ---------------------------------------------------------------------------------------------
+struct QArgs {
+  int kind, hq, wq, mirror, L;
+  float hmax, clampv, tau, iter_frac, c_s, s, beta, phase_scale;
+  float lut[THZ_MAX_LUT];
+  float plut_w[THZ_MAX_LUT];  // wrapped phase LUT (SGV3)
+};
+
+__device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+#pragma clang fp contract(off)
+// torch.remainder(a, b) for b > 0 (fmod with the sign of the divisor)
+__device__ __forceinline__ float rem_pos(float a, float b) {
+  float m = fmodf(a, b);
+  if (m != 0.0f && m < 0.0f) m += b;
+  return m;
+}
+__device__ __forceinline__ float wrap_pi(float x) {
+  const float PI = 3.1415927410125732f, TWO_PI = 6.2831854820251465f;
+  return rem_pos(x + PI, TWO_PI) - PI;
+}
+// SGV3 scores (score_phase(func='sigmoid') * c_s * s, :794-817, :833) and d score / d phase
+__device__ __forceinline__ void sgv3_score(const QArgs& a, float phase, int l, float* score, float* dscore) {
+  const float PI = 3.1415927410125732f, TWO_PI = 6.2831854820251465f;
+  const float wp = wrap_pi(phase);
+  float d = wp - a.plut_w[l];
+  d = rem_pos(d + PI, TWO_PI) - PI;
+  d = d / PI;
+  const float z = a.s * d;
+  const float sg = sigm(z);
+  const float sc = sg * (1.0f - sg) * 4.0f;
+  *score = (sc * a.c_s) * a.s;
+  // d/dphase: 4 sg (1-sg)(1-2sg) * s/pi * c_s * s
+  *dscore = 4.0f * sg * (1.0f - sg) * (1.0f - 2.0f * sg) * (a.s / PI) * a.c_s * a.s;
+}
+
+// quadrant pixel (i, j) -> its up to four mirror positions in the full map (:28-35)
+template <class F>
+__device__ __forceinline__ void for_mirrors(const QArgs& a, int i, int j, F fn) {
+  if (!a.mirror) {
+    fn(i * a.wq + j);
+    return;
+  }
+  const int W = 2 * a.wq;
+  const int r0 = a.hq - 1 - i, r1 = a.hq + i;
+  const int c0 = a.wq - 1 - j, c1 = a.wq + j;
+  fn(r0 * W + c0);
+  fn(r0 * W + c1);
+  fn(r1 * W + c0);
+  fn(r1 * W + c1);
+}
+
+// gumbel_softmax(logits, tau, hard) over L values: returns the hard index, y_soft in y
+__device__ __forceinline__ int gumbel_soft(const float* logits, const float* expo, int L, float tau, float* y) {
+  float mx = -INFINITY;
+  for (int l = 0; l < L; ++l) {
+    y[l] = (logits[l] + (-logf(expo[l]))) / tau;
+    mx = fmaxf(mx, y[l]);
+  }
+  float sum = 0.f;
+  for (int l = 0; l < L; ++l) {
+    y[l] = expf(y[l] - mx);
+    sum += y[l];
+  }
+  int arg = 0;
+  float best = -1.f;
+  for (int l = 0; l < L; ++l) {
+    y[l] = y[l] / sum;
+    if (y[l] > best) {
+      best = y[l];
+      arg = l;
+    }
+  }
+  return arg;
+}
+
+// straight-through value sum_l lut_l * ((onehot_l - y_l) + y_l)
+__device__ __forceinline__ float st_value(const QArgs& a, const float* y, int arg) {
+  float q = 0.f;
+  for (int l = 0; l < a.L; ++l) q += a.lut[l] * (((l == arg ? 1.0f : 0.0f) - y[l]) + y[l]);
+  return q;
+}
+
+__global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __restrict__ expo,
+                          float* __restrict__ hfull, float* __restrict__ ysave) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.hq * a.wq;
+  if (p >= n) return;
+  const int i = p / a.wq, j = p - i * a.wq;
+  float out;
+  float y[THZ_MAX_LUT];
+  if (a.kind == THZ_Q_NGS) {
+    const int arg = gumbel_soft(w + (size_t)p * a.L, expo + (size_t)p * a.L, a.L, a.tau, y);
+    out = st_value(a, y, arg);
+    for (int l = 0; l < a.L; ++l) ysave[(size_t)p * a.L + l] = y[l];
+  } else if (a.kind == THZ_Q_SGV1) {
+    // the weight is the phase itself (:411-445): scores of w, Gumbel pick, LUT value
+    float logits[THZ_MAX_LUT], ex[THZ_MAX_LUT];
+    for (int l = 0; l < a.L; ++l) {
+      float dsc;
+      sgv3_score(a, w[p], l, &logits[l], &dsc);
+      ex[l] = expo[(size_t)l * n + p];
+    }
+    const int arg = gumbel_soft(logits, ex, a.L, a.tau, y);
+    out = st_value(a, y, arg);
+    for (int l = 0; l < a.L; ++l) ysave[(size_t)l * n + p] = y[l];
+  } else {
+    const float wc = fminf(fmaxf(w[p], -a.clampv), a.clampv);
+    const float hm = a.hmax * sigm(wc);
+    out = hm;
+    if (a.kind == THZ_Q_STE) {
+      int arg = 0;
+      float best = INFINITY;
+      for (int l = 0; l < a.L; ++l) {
+        const float dd = fabsf(hm - a.lut[l]);
+        if (dd < best) {
+          best = dd;
+          arg = l;
+        }
+      }
+      out = a.lut[arg];
+    } else if (a.kind == THZ_Q_PSQ) {
+      const float delta = (a.hmax - 0.0f) / (float)(a.L - 1);
+      const float xn = (hm - 0.0f) / delta - 0.5f;
+      float sm = 0.f;
+      for (int l = 0; l < a.L - 1; ++l) sm += sigm(a.tau * (xn - (float)l));
+      out = 0.0f + delta * sm;
+    } else if (a.kind == THZ_Q_SGV3 && a.iter_frac > 0.3f) {
+      const float phase = a.phase_scale * hm;
+      float logits[THZ_MAX_LUT], ex[THZ_MAX_LUT];
+      for (int l = 0; l < a.L; ++l) {
+        float dsc;
+        sgv3_score(a, phase, l, &logits[l], &dsc);
+        ex[l] = expo[(size_t)l * n + p];
+      }
+      const int arg = gumbel_soft(logits, ex, a.L, a.tau, y);
+      const float q = st_value(a, y, arg);
+      out = a.iter_frac <= 0.8f ? (1.0f - a.beta) * hm + a.beta * q : q;
+      for (int l = 0; l < a.L; ++l) ysave[(size_t)l * n + p] = y[l];
+    }
+  }
+  for_mirrors(a, i, j, [&](int o) { hfull[o] = out; });
+}
+
+__global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __restrict__ ysave,
+                          const float* __restrict__ gfull, float* __restrict__ gw) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.hq * a.wq;
+  if (p >= n) return;
+  const int i = p / a.wq, j = p - i * a.wq;
+  float G = 0.f;
+  for_mirrors(a, i, j, [&](int o) { G += gfull[o]; });
+  if (a.kind == THZ_Q_NGS) {
+    // d logits_l = y_l (dy_l - sum_k y_k dy_k) / tau, dy_l = G lut_l
+    float dot = 0.f;
+    for (int l = 0; l < a.L; ++l) dot += ysave[(size_t)p * a.L + l] * G * a.lut[l];
+    for (int l = 0; l < a.L; ++l) {
+      const float yl = ysave[(size_t)p * a.L + l];
+      gw[(size_t)p * a.L + l] = yl * (G * a.lut[l] - dot) / a.tau;
+    }
+    return;
+  }
+  if (a.kind == THZ_Q_SGV1) {
+    float dot = 0.f;
+    for (int l = 0; l < a.L; ++l) dot += ysave[(size_t)l * n + p] * G * a.lut[l];
+    float dphase = 0.f;
+    for (int l = 0; l < a.L; ++l) {
+      const float yl = ysave[(size_t)l * n + p];
+      float sc, dsc;
+      sgv3_score(a, w[p], l, &sc, &dsc);
+      dphase += yl * (G * a.lut[l] - dot) / a.tau * dsc;
+    }
+    gw[p] = dphase;
+    return;
+  }
+  const float wv = w[p];
+  const float wc = fminf(fmaxf(wv, -a.clampv), a.clampv);
+  const float sg = sigm(wc);
+  const float hm = a.hmax * sg;
+  float dhm = G;  // FP and STE (identity straight-through)
+  if (a.kind == THZ_Q_PSQ) {
+    const float delta = (a.hmax - 0.0f) / (float)(a.L - 1);
+    const float xn = (hm - 0.0f) / delta - 0.5f;
+    float d = 0.f;
+    for (int l = 0; l < a.L - 1; ++l) {
+      const float s2 = sigm(a.tau * (xn - (float)l));
+      d += s2 * (1.0f - s2) * a.tau;
+    }
+    dhm = G * d;  // delta * sum(tau sig') / delta
+  } else if (a.kind == THZ_Q_SGV3 && a.iter_frac > 0.3f) {
+    const bool blend = a.iter_frac <= 0.8f;
+    const float gq = blend ? a.beta * G : G;
+    float dot = 0.f;
+    for (int l = 0; l < a.L; ++l) dot += ysave[(size_t)l * n + p] * gq * a.lut[l];
+    const float phase = a.phase_scale * hm;
+    float dphase = 0.f;
+    for (int l = 0; l < a.L; ++l) {
+      const float yl = ysave[(size_t)l * n + p];
+      const float dlogit = yl * (gq * a.lut[l] - dot) / a.tau;
+      float sc, dsc;
+      sgv3_score(a, phase, l, &sc, &dsc);
+      dphase += dlogit * dsc;
+    }
+    dhm = (blend ? (1.0f - a.beta) * G : 0.0f) + dphase * a.phase_scale;
+  }
+  const bool inside = wv >= -a.clampv && wv <= a.clampv;  // clamp passes the gradient on [min, max]
+  gw[p] = inside ? dhm * a.hmax * sg * (1.0f - sg) : 0.0f;
+}
+
+static int qargs(const thz_quant_desc* d, QArgs* a) {
+  if (!d) return fail(THZ_E_ARG, "null descriptor");
+  if (d->kind < THZ_Q_FP || d->kind > THZ_Q_SGV1) return fail(THZ_E_ARG, "bad quantizer kind %d", d->kind);
+  if (d->hq < 1 || d->wq < 1) return fail(THZ_E_ARG, "bad quantizer size");
+  if (d->L < 1 || d->L > THZ_MAX_LUT) return fail(THZ_E_UNSUPPORTED, "LUT levels %d outside [1, %d]", d->L, THZ_MAX_LUT);
+  if (!d->lut) return fail(THZ_E_ARG, "null LUT");
+  if (d->kind == THZ_Q_PSQ && d->L < 2) return fail(THZ_E_ARG, "PSQ needs >= 2 levels");
+  a->kind = d->kind;
+  a->hq = d->hq;
+  a->wq = d->wq;
+  a->mirror = d->mirror;
+  a->L = d->L;
+  a->hmax = d->hmax;
+  a->clampv = d->clamp;
+  a->tau = d->tau;
+  a->iter_frac = d->iter_frac;
+  a->c_s = d->c_s;
+  a->s = d->s;
+  a->beta = d->beta;
+  a->phase_scale = d->phase_scale;
+  for (int l = 0; l < d->L; ++l) {
+    a->lut[l] = d->lut[l];
+    // (phase_lut + pi) % 2pi - pi of the reference's LUT phases (:802), host fp32
+    const float PI = 3.1415927410125732f, TWO_PI = 6.2831854820251465f;
+    const float ph = d->phase_scale * d->lut[l];
+    float m = std::fmod(ph + PI, TWO_PI);
+    if (m != 0.0f && m < 0.0f) m += TWO_PI;
+    a->plut_w[l] = m - PI;
+  }
+  return THZ_OK;
+}
+
+}  // namespace thz
+
+using namespace thz;
+
+extern "C" int thz_doe_modulate_forward(const thz_doe_desc* d, const void* field, const float* height,
+                                        const float* noise, void* out, float* height_full, thz_stream_t stream) {
+  if (!d || !field || !height || !out) return fail(THZ_E_ARG, "null argument");
+  if (d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1 || d->hs < 1 || d->ws < 1) return fail(THZ_E_ARG, "bad shape");
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  ModArgs a{};
+  a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W; a.hs = d->hs; a.ws = d->ws;
+  a.has_noise = noise != nullptr;
+  a.tol = d->tolerance; a.eps = d->epsilon; a.tand = d->tand;
+  for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("doe_modulate_fwd", s);
+  const int n = d->H * d->W;
+  hipLaunchKernelGGL(doe_modulate_fwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)field, height, noise,
+                     (float2*)out, height_full, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_doe_modulate_backward(const thz_doe_desc* d, const void* grad_out, const void* field,
+                                         const float* height, const float* noise, void* grad_field,
+                                         float* grad_height, thz_stream_t stream) {
+  if (!d || !grad_out || !field || !height) return fail(THZ_E_ARG, "null argument");
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  ModArgs a{};
+  a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W; a.hs = d->hs; a.ws = d->ws;
+  a.has_noise = noise != nullptr;
+  a.tol = d->tolerance; a.eps = d->epsilon; a.tand = d->tand;
+  for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("doe_modulate_bwd", s);
+  if (grad_height && (d->hs != d->H || d->ws != d->W))
+    THZ_HIP_CHECK(hipMemsetAsync(grad_height, 0, sizeof(float) * d->hs * d->ws, s));
+  const int n = d->H * d->W;
+  hipLaunchKernelGGL(doe_modulate_bwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)grad_out,
+                     (const float2*)field, height, noise, (float2*)grad_field, grad_height, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_quant_forward(const thz_quant_desc* d, const float* weight, const float* noise_exp,
+                                 float* height_full, float* y_soft, thz_stream_t stream) {
+  QArgs a;
+  int e = qargs(d, &a);
+  if (e) return e;
+  const bool gumbel =
+      d->kind == THZ_Q_NGS || d->kind == THZ_Q_SGV1 || (d->kind == THZ_Q_SGV3 && d->iter_frac > 0.3f);
+  if (!weight || !height_full || (gumbel && (!noise_exp || !y_soft)))
+    return fail(THZ_E_ARG, "null argument (Gumbel kinds need noise_exp and y_soft)");
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("quant_fwd", s);
+  const int n = d->hq * d->wq;
+  hipLaunchKernelGGL(quant_fwd, dim3((n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_quant_backward(const thz_quant_desc* d, const float* weight, const float* y_soft,
+                                  const float* grad_full, float* grad_weight, thz_stream_t stream) {
+  QArgs a;
+  int e = qargs(d, &a);
+  if (e) return e;
+  if (!weight || !grad_full || !grad_weight) return fail(THZ_E_ARG, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("quant_bwd", s);
+  const int n = d->hq * d->wq;
+  hipLaunchKernelGGL(quant_bwd, dim3((n + 255) / 256), dim3(256), 0, s, a, weight, y_soft, grad_full, grad_weight);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Rotationally symmetric layers (QuantizedDOE.py:1399-1623): radial profile [R] -> quadrant
+// bins floor(sqrt(x^2 + y^2)) (< R-1, else 0) -> mirrored 2R x 2R map -> centre crop [H, W].
+// ---------------------------------------------------------------------------------------------
+namespace thz {
+__device__ __forceinline__ int radial_bin(int i, int j, int R, int H, int W) {
+  const int fi = R - H / 2 + i, fj = R - W / 2 + j;  // centre crop start (:1427-1429)
+  const int qx = fi < R ? R - 1 - fi : fi - R;
+  const int qy = fj < R ? R - 1 - fj : fj - R;
+  const float d = sqrtf((float)(qx * qx + qy * qy));
+  return d < (float)(R - 1) ? (int)floorf(d) : -1;
+}
+
+__global__ void radial_fwd(const float* __restrict__ prof, float* __restrict__ out, int R, int H, int W) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= H * W) return;
+  const int b = radial_bin(p / W, p % W, R, H, W);
+  out[p] = b >= 0 ? prof[b] : 0.0f;
+}
+
+__global__ void radial_bwd(const float* __restrict__ g, float* __restrict__ gprof, int R, int H, int W) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= H * W) return;
+  const int b = radial_bin(p / W, p % W, R, H, W);
+  if (b >= 0) atomicAdd(gprof + b, g[p]);
+}
+}  // namespace thz
+
+extern "C" int thz_radial_forward(const float* profile, int R, int H, int W, float* out, thz_stream_t stream) {
+  if (!profile || !out || R < 2 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
+    return fail(THZ_E_ARG, "bad radial map arguments R=%d H=%d W=%d", R, H, W);
+  hipLaunchKernelGGL(radial_fwd, dim3((H * W + 255) / 256), dim3(256), 0, (hipStream_t)stream, profile, out, R, H, W);
+  THZ_LAUNCH_CHECK();
+  return THZ_OK;
+}
+
+extern "C" int thz_radial_backward(const float* grad_out, int R, int H, int W, float* grad_profile,
+                                   thz_stream_t stream) {
+  if (!grad_out || !grad_profile || R < 2 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
+    return fail(THZ_E_ARG, "bad radial map arguments");
+  hipStream_t s = (hipStream_t)stream;
+  THZ_HIP_CHECK(hipMemsetAsync(grad_profile, 0, sizeof(float) * R, s));
+  hipLaunchKernelGGL(radial_bwd, dim3((H * W + 255) / 256), dim3(256), 0, s, grad_out, grad_profile, R, H, W);
+  THZ_LAUNCH_CHECK();
+  return THZ_OK;
+}

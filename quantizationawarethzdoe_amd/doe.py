@@ -1,0 +1,169 @@
+"""Device entry points for the DOE layers: torch.autograd glue over the C-ABI (thz_doe.hip).
+
+All compute runs in libthzdoe's kernels; torch allocates the buffers and draws the random
+numbers the reference draws (``rand_like`` height noise, ``exponential_`` Gumbel noise) so
+the same generator state reproduces the reference's RNG stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .propagation import _require_device, _stream_handle
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths):
+    wl = _lib.float_array(wavelengths)
+    d = _lib.DoeDesc(B=B, C=C, H=H, W=W, hs=hs, ws=ws, tolerance=float(tol), epsilon=float(eps), tand=float(tand),
+                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)))
+    d._keep = wl
+    return d
+
+
+class _Modulate(torch.autograd.Function):
+    """field * t(h + noise), nearest-upsampled (Components/QuantizedDOE.py:92-126)."""
+
+    @staticmethod
+    def forward(ctx, field, height, noise, tol, eps, tand, wavelengths):
+        _require_device(field, "DOE modulate")
+        field = field.contiguous()
+        height = height.detach().contiguous().float()
+        B, C, H, W = field.shape
+        hs, ws = height.shape
+        d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths)
+        out = torch.empty_like(field)
+        hfull = torch.empty((H, W), dtype=torch.float32, device=field.device)
+        with torch.cuda.device(field.device):
+            _lib.check(_lib.lib().thz_doe_modulate_forward(ctypes.byref(d), _ptr(field), _ptr(height), _ptr(noise),
+                                                           _ptr(out), _ptr(hfull), _stream_handle()))
+        ctx.save_for_backward(field, height, noise)
+        ctx.cfg = (tol, eps, tand, wavelengths)
+        ctx.mark_non_differentiable(hfull)
+        return out, hfull
+
+    @staticmethod
+    def backward(ctx, g, _gh):
+        field, height, noise = ctx.saved_tensors
+        tol, eps, tand, wavelengths = ctx.cfg
+        B, C, H, W = field.shape
+        hs, ws = height.shape
+        d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths)
+        g = g.contiguous()
+        gf = torch.empty_like(field) if ctx.needs_input_grad[0] else None
+        gh = torch.empty((hs, ws), dtype=torch.float32, device=field.device) if ctx.needs_input_grad[1] else None
+        with torch.cuda.device(field.device):
+            _lib.check(_lib.lib().thz_doe_modulate_backward(ctypes.byref(d), _ptr(g), _ptr(field), _ptr(height),
+                                                            _ptr(noise), _ptr(gf), _ptr(gh), _stream_handle()))
+        return gf, gh, None, None, None, None, None
+
+
+def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None):
+    """Differentiable DOE modulation on the HIP kernel; returns (out, noisy full-size height)."""
+    if field.dtype != torch.complex64:
+        raise TypeError(f"DOE kernels compute in complex64; got {field.dtype}")
+    if tolerance is not None and noise is None:
+        noise = torch.rand_like(height)
+    if noise is not None:
+        noise = noise.detach().contiguous().float()
+    tol = 0.0 if tolerance is None else float(tolerance)
+    return _Modulate.apply(field, height, noise, tol, float(eps), float(tand), tuple(map(float, wavelengths)))
+
+
+def _quant_desc(kind, hq, wq, mirror, lut, hmax, clamp, tau=1.0, iter_frac=0.0, c_s=0.0, s=0.0, beta=0.0,
+                phase_scale=0.0):
+    arr = _lib.float_array(lut)
+    d = _lib.QuantDesc(kind=kind, hq=hq, wq=wq, mirror=int(bool(mirror)), L=len(lut),
+                       lut=ctypes.cast(arr, ctypes.POINTER(ctypes.c_float)), hmax=float(hmax), clamp=float(clamp),
+                       tau=float(tau), iter_frac=float(iter_frac), c_s=float(c_s), s=float(s), beta=float(beta),
+                       phase_scale=float(phase_scale))
+    d._keep = arr
+    return d
+
+
+class _Quantize(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, weight, expo, cfg):
+        kind, hq, wq, mirror, lut, kw = cfg
+        d = _quant_desc(kind, hq, wq, mirror, lut, **kw)
+        w = weight.detach().contiguous().float()
+        Hf, Wf = (2 * hq, 2 * wq) if mirror else (hq, wq)
+        out = torch.empty((Hf, Wf), dtype=torch.float32, device=w.device)
+        ysoft = torch.empty_like(expo) if expo is not None else None
+        with torch.cuda.device(w.device):
+            _lib.check(_lib.lib().thz_quant_forward(ctypes.byref(d), _ptr(w), _ptr(expo), _ptr(out), _ptr(ysoft),
+                                                    _stream_handle()))
+        ctx.save_for_backward(w, ysoft)
+        ctx.cfg = cfg
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        w, ysoft = ctx.saved_tensors
+        kind, hq, wq, mirror, lut, kw = ctx.cfg
+        d = _quant_desc(kind, hq, wq, mirror, lut, **kw)
+        gw = torch.empty_like(w)
+        with torch.cuda.device(w.device):
+            _lib.check(_lib.lib().thz_quant_backward(ctypes.byref(d), _ptr(w), _ptr(ysoft), _ptr(g.contiguous()),
+                                                     _ptr(gw), _stream_handle()))
+        return gw, None, None
+
+
+def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, **kw):
+    """Quantized height map of one of the QAT layers (HIP forward + backward); weight shape kept."""
+    _require_device(weight, "DOE quantizer")
+    shape = weight.shape
+    if kind == _lib.Q_NGS:
+        hq, wq = shape[-3], shape[-2]  # logits [.., hq, wq, L]
+    elif weight.dim() == 1:
+        hq, wq = 1, shape[0]  # radial profile
+    else:
+        hq, wq = shape[-2], shape[-1]
+    if len(lut) > _lib.THZ_MAX_LUT:
+        raise ValueError(f"at most {_lib.THZ_MAX_LUT} LUT levels")
+    cfg = (kind, int(hq), int(wq), bool(mirror), tuple(float(v) for v in lut),
+           dict(hmax=float(hmax), clamp=float(clamp), **{k: float(v) for k, v in kw.items()}))
+    e = expo.contiguous().float() if expo is not None else None
+    return _Quantize.apply(weight.reshape(shape), e, cfg)
+
+
+class _Radial(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, prof, R, H, W):
+        p = prof.detach().contiguous().float().reshape(-1)
+        out = torch.empty((H, W), dtype=torch.float32, device=p.device)
+        with torch.cuda.device(p.device):
+            _lib.check(_lib.lib().thz_radial_forward(_ptr(p), R, H, W, _ptr(out), _stream_handle()))
+        ctx.cfg = (prof.shape, R, H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        shape, R, H, W = ctx.cfg
+        gp = torch.empty(R, dtype=torch.float32, device=g.device)
+        with torch.cuda.device(g.device):
+            _lib.check(_lib.lib().thz_radial_backward(_ptr(g.contiguous()), R, H, W, _ptr(gp), _stream_handle()))
+        return gp.reshape(shape), None, None, None
+
+
+def radial_map(profile, H, W):
+    """Radial profile [.., R] -> [H, W] height map (Components/QuantizedDOE.py:1409-1433)."""
+    _require_device(profile, "radial map")
+    return _Radial.apply(profile, int(profile.shape[-1]), int(H), int(W))
+
+
+def f32(x):
+    return float(np.float32(x))
+
+
+def phase_scale(lam_min, eps):
+    """fp32 (2 pi / lambda) * (sqrt(eps) - 1), the height->phase factor (QuantizedDOE.py:40-41)."""
+    k = np.float32(2 * math.pi) / np.float32(lam_min)
+    return float(np.float32(k) * (np.sqrt(np.float32(eps)) - np.float32(1)))

@@ -313,14 +313,111 @@ def gen_doe(manifest):
     np.savez_compressed(os.path.join(HERE, "doe_golden.npz"), **arrays)
 
 
+@contextlib.contextmanager
+def record_rng():
+    """Record every exponential_ / rand_like draw the reference makes, in order."""
+    draws = []
+    orig_exp, orig_rl = torch.Tensor.exponential_, torch.rand_like
+
+    def exp_(self, *a, **k):
+        r = orig_exp(self, *a, **k)
+        draws.append(("expo", r.detach().clone().numpy()))
+        return r
+
+    def rand_like(t, *a, **k):
+        r = orig_rl(t, *a, **k)
+        draws.append(("unif", r.detach().clone().numpy()))
+        return r
+
+    torch.Tensor.exponential_, torch.rand_like = exp_, rand_like
+    try:
+        yield draws
+    finally:
+        torch.Tensor.exponential_, torch.rand_like = orig_exp, orig_rl
+
+
+DOE_LAYER_CASES = [
+    # name, class, num_unit, iter_frac, optim_params overrides, look_up_table
+    ("fp_unit", "FullPrecisionDOELayer", 2, None, None, None),
+    ("fp_full", "FullPrecisionDOELayer", None, None, None, None),
+    ("ste_unit", "STEQuantizedDOELayer", 2, None, None, None),
+    ("ste_full", "STEQuantizedDOELayer", None, None, None, None),
+    ("psq_full", "PSQuantizedDOELayer", None, 0.5, dict(tau_max=20, tau_min=1), None),
+    ("psq_unit", "PSQuantizedDOELayer", 2, 0.2, dict(tau_max=20, tau_min=1), None),
+    ("ngs_unit", "NaiveGumbelQuantizedDOELayer", 2, 0.5, None, None),
+    ("ngs_full", "NaiveGumbelQuantizedDOELayer", None, 0.9, None, None),
+    ("v1_full", "SoftGumbelQuantizedDOELayer", None, 0.5, None, None),
+    ("v2_cont", "SoftGumbelQuantizedDOELayerv2", None, 0.3, None, None),
+    ("v2_quant", "SoftGumbelQuantizedDOELayerv2", None, 0.7, None, None),
+    ("v3_full", "SoftGumbelQuantizedDOELayerv3", None, 0.6, None, None),
+    ("v3_lut", "SoftGumbelQuantizedDOELayerv3", 2, 0.95, None, [0.0, 0.2e-3, 0.5e-3, 0.9e-3]),
+    ("rs_fp", "RotationallySymmetricFullPrecisionDOELayer", None, None, None, None),
+    ("rs_v3_blend", "RotationallySymmetricScoreGumbelSoftQuantizedDOELayer", None, 0.5, None, None),
+    ("rs_v3_quant", "RotationallySymmetricScoreGumbelSoftQuantizedDOELayer", None, 0.9, None, None),
+    ("rs_ste", "RotationallySymmetricSTEQuantizedDOELayer", None, None, None, None),
+    ("rs_ngs", "RotationallySymmetricNaiveGumbelQuantizedDOELayer", None, 0.5, None, None),
+    ("rs_psq", "RotationallySymmetricPSQuantizedQuantizedDOELayer", None, 0.5, dict(tau_max=20, tau_min=1), None),
+]
+
+
+def gen_doe_layers(manifest):
+    """Every other QAT layer: forward height map + field and the weight gradient of sum |E|^2,
+    with the RNG draws the reference made recorded in order."""
+    arrays = {}
+    freqs = [300, 320]
+    wl = [C0 / (g * 1e9) for g in freqs]
+    x = rand_field((1, 2, 32, 32), 31)
+    arrays["in"] = x
+    manifest["doe_layers"] = []
+    for name, cls, num_unit, iter_frac, opt, lut in DOE_LAYER_CASES:
+        doe_params = dict(doe_size=[32, 32], doe_dxy=1 * MM, doe_level=4, num_unit=num_unit,
+                          height_constraint_max=1 * MM, tolerance=0.01 * MM, material=[EPS, TAND])
+        if lut is not None:
+            doe_params["look_up_table"] = lut
+        optim_params = dict(c_s=100, tau_max=2.5, tau_min=1.5)
+        optim_params.update(opt or {})
+        torch.manual_seed(5)
+        klass = getattr(ref.DOE, cls)
+        layer = klass(doe_params, device="cpu") if cls.endswith("FullPrecisionDOELayer") \
+            else klass(doe_params, optim_params, device="cpu")
+        pname, param = next(iter(layer.named_parameters()))
+        w = param.detach().numpy().copy()
+        field = make_field(x, wl_arg(wl), [1 * MM, 1 * MM], False)
+        torch.manual_seed(77)
+        with record_rng() as draws:
+            out = layer(field, iter_frac=iter_frac)
+        loss = (out.data.abs() ** 2).sum()
+        loss.backward()
+        arrays.update({f"{name}__w": w, f"{name}__out32": out.data.detach().numpy(),
+                       f"{name}__hmap": layer.height_map.detach().numpy().copy(),
+                       f"{name}__gw": param.grad.numpy().copy()})
+        kinds = []
+        for i, (kind, val) in enumerate(draws):
+            arrays[f"{name}__draw{i}"] = val
+            kinds.append(kind)
+        manifest["doe_layers"].append(dict(name=name, cls=cls, param=pname, iter_frac=iter_frac,
+                                           doe_params=doe_params, optim_params=optim_params, f=freqs,
+                                           draws=kinds, loss="sum |E|^2"))
+        print("doe_layer", name, pname, w.shape, kinds)
+    np.savez_compressed(os.path.join(HERE, "doe_layers_golden.npz"), **arrays)
+
+
 def main():
-    manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
-                "asm": [], "czt": [], "rsc": [], "doe": []}
-    gen_asm(manifest)
-    gen_asm_cfg1(manifest)
-    gen_czt_rsc(manifest)
-    gen_doe(manifest)
-    with open(os.path.join(HERE, "manifest.json"), "w") as fh:
+    path = os.path.join(HERE, "manifest.json")
+    if "--only" in sys.argv:
+        which = sys.argv[sys.argv.index("--only") + 1]
+        with open(path) as fh:
+            manifest = json.load(fh)
+        {"doe_layers": gen_doe_layers}[which](manifest)
+    else:
+        manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
+                    "asm": [], "czt": [], "rsc": [], "doe": []}
+        gen_asm(manifest)
+        gen_asm_cfg1(manifest)
+        gen_czt_rsc(manifest)
+        gen_doe(manifest)
+        gen_doe_layers(manifest)
+    with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1, default=float)
 
 

@@ -52,3 +52,57 @@ def test_cpu_tensor_is_rejected():
     from quantizationawarethzdoe_amd import propagation as P
     with pytest.raises(RuntimeError, match="ROCm device"):
         P.asm_apply(torch.zeros(1, 1, 8, 8, dtype=torch.complex64), [1e-3], [1e-3, 1e-3], [0.1], 4, 4, True, 1)
+
+
+def test_quantizer_descriptor_validation_without_gpu():
+    from quantizationawarethzdoe_amd import _lib, doe
+    L = ctypes.c_void_p(0)
+    bad_kind = doe._quant_desc(9, 4, 4, False, [0.0, 1.0], 1.0, 8.0)
+    code = _lib.lib().thz_quant_forward(ctypes.byref(bad_kind), L, L, L, L, L)
+    assert code == _lib.THZ_E_ARG and b"kind" in _lib.lib().thz_last_error()
+    too_many = doe._quant_desc(_lib.Q_STE, 4, 4, False, [0.1 * i for i in range(17)], 1.0, 8.0)
+    assert _lib.lib().thz_quant_forward(ctypes.byref(too_many), L, L, L, L, L) == _lib.THZ_E_UNSUPPORTED
+    psq1 = doe._quant_desc(_lib.Q_PSQ, 4, 4, False, [0.0], 1.0, 8.0)
+    assert _lib.lib().thz_quant_backward(ctypes.byref(psq1), L, L, L, L, L) == _lib.THZ_E_ARG
+    # Gumbel kinds need the Exp(1) draw
+    ngs = doe._quant_desc(_lib.Q_NGS, 4, 4, False, [0.0, 1.0], 1.0, 8.0)
+    w = ctypes.c_void_p(8)
+    assert _lib.lib().thz_quant_forward(ctypes.byref(ngs), w, L, w, L, L) == _lib.THZ_E_ARG
+
+
+def test_doe_layers_construct_on_cpu_and_fail_loudly():
+    """The QAT layer mirrors keep the reference's parameter shapes; compute refuses CPU tensors."""
+    import torch
+    from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    dp = dict(doe_size=[100, 100], doe_dxy=1e-3, doe_level=4, num_unit=2, height_constraint_max=1e-3,
+              tolerance=1e-5, material=[2.66, 0.03])
+    op = dict(c_s=100, tau_max=2.5, tau_min=1.5)
+    shapes = {
+        "FullPrecisionDOELayer": (1, 1, 50, 50), "STEQuantizedDOELayer": (1, 1, 50, 50),
+        "PSQuantizedDOELayer": (50, 50), "NaiveGumbelQuantizedDOELayer": (50, 50, 4),
+        "SoftGumbelQuantizedDOELayer": (1, 1, 50, 50), "SoftGumbelQuantizedDOELayerv3": (50, 50),
+        "RotationallySymmetricFullPrecisionDOELayer": (70,),
+        "RotationallySymmetricScoreGumbelSoftQuantizedDOELayer": (1, 1, 1, 70),
+        "RotationallySymmetricSTEQuantizedDOELayer": (1, 70),
+        "RotationallySymmetricNaiveGumbelQuantizedDOELayer": (1, 70, 4),
+        "RotationallySymmetricPSQuantizedQuantizedDOELayer": (1, 70),
+    }
+    for name, shape in shapes.items():
+        k = getattr(Q, name)
+        layer = k(dp, device="cpu") if name.endswith("FullPrecisionDOELayer") else k(dp, op, device="cpu")
+        p = next(iter(layer.parameters()))
+        assert tuple(p.shape) == shape, (name, p.shape)
+    assert Q.SoftGumbelQuantizedDOELayerv3(dp, op, device="cpu").lut.tolist() == \
+        torch.linspace(0, torch.tensor(1e-3), 5)[:-1].tolist()
+    field = ElectricField(torch.ones(1, 1, 100, 100, dtype=torch.complex64), wavelengths=1e-3,
+                          spacing=[1e-3, 1e-3], device="cpu")
+    layer = Q.SoftGumbelQuantizedDOELayerv3(dp, op, device="cpu")
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        layer(field, iter_frac=0.9)
+
+
+def test_tau_schedules():
+    from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+    assert Q._cos_tau(0.0, 1.5, 2.5) == 2.5 and Q._cos_tau(1.0, 1.5, 2.5) == 1.5
+    assert Q._linear_tau(0.5, 1, 401) == 201

@@ -159,3 +159,39 @@ def test_ste_kat():
     """STE KAT: [0.1,0.4,0.7,1.2] on LUT [0,.5,1] -> [0,.5,.5,1] (Components/test_all.ipynb:595-606)."""
     q = orc.ste_quantize(torch.tensor([0.1, 0.4, 0.7, 1.2]), torch.tensor([0.0, 0.5, 1.0]))
     assert q.tolist() == [0.0, 0.5, 0.5, 1.0]
+
+
+LAYERS = M.get("doe_layers", [])
+
+
+def layer_inputs(case):
+    """Weight, LUT, wavelengths and the recorded RNG draws of one doe_layers fixture."""
+    A = arrays("doe_layers")
+    k = case["name"]
+    dp = case["doe_params"]
+    if dp.get("look_up_table") is not None:
+        lut = torch.tensor(dp["look_up_table"], dtype=torch.float32)
+    else:
+        lut = torch.linspace(0, torch.tensor(dp["height_constraint_max"]), dp["doe_level"] + 1)[:-1]
+    draws = {kind: A[f"{k}__draw{i}"] for i, kind in enumerate(case["draws"])}
+    return A, k, dp, lut, draws
+
+
+@pytest.mark.parametrize("case", LAYERS, ids=[c["name"] for c in LAYERS])
+def test_doe_layer_oracle_matches_reference(case):
+    A, k, dp, lut, draws = layer_inputs(case)
+    w = torch.from_numpy(A[f"{k}__w"]).requires_grad_(True)
+    lam = wavelengths(case["f"], False)
+    expo = torch.from_numpy(draws["expo"]) if "expo" in draws else None
+    h = orc.layer_height_map(case["cls"], w, lut, torch.tensor(dp["height_constraint_max"]), lam.min(),
+                             dp["material"][0], case["iter_frac"], case["optim_params"], dp["num_unit"],
+                             dp["doe_size"], expo=expo)
+    np.testing.assert_allclose(h.detach().numpy(), A[f"{k}__hmap"], rtol=1e-6, atol=1e-12)
+    x = torch.from_numpy(A["in"])
+    mat = torch.tensor(dp["material"])
+    out = orc.doe_modulate(x, h, lam, mat[0], mat[1], tolerance=dp["tolerance"],
+                           noise_u01=torch.from_numpy(draws["unif"]))
+    assert rel_l2(out.detach().numpy(), A[f"{k}__out32"]) <= 1e-6
+    (out.abs() ** 2).sum().backward()
+    g = A[f"{k}__gw"]
+    assert rel_l2(w.grad.numpy(), g) <= 1e-5 or np.abs(g).max() == np.abs(w.grad.numpy()).max() == 0
