@@ -35,17 +35,29 @@ METRIC = "complex-field propagations/sec (N×N) + achieved HBM GB/s at 1/2/4/8 G
 
 
 def gaussian(N, dx, w, device):
-    """Gaussian_beam (LightSource/Gaussian_beam.py:88-160) at its waist (z_w0 = 0, R = 1e12):
-    amplitude exp(-(x^2+y^2)/w^2); the 1e12 m curvature phase (< 1e-8 rad) is dropped."""
-    xs = torch.linspace(-dx * N / 2, dx * N / 2, N, device=device, dtype=torch.float32)
-    X, Y = torch.meshgrid(xs, xs, indexing="ij")
-    return torch.exp(-(X * X) / (w * w) - (Y * Y) / (w * w)).to(torch.complex64)[None, None]
+    """Guassian_beam (LightSource/Gaussian_beam.py:88-160) at its waist, generated on the device
+    by the thz_gaussian_beam kernel (CPU sample: the oracle's restatement)."""
+    lam = C0 / FREQ
+    if torch.device(device).type == "cpu":
+        from oracle import thz_oracle as orc
+        d = torch.tensor(dx, dtype=torch.float32)
+        return orc.gaussian_beam(N, N, d, d, torch.tensor([lam], dtype=torch.float32), w, w).to(torch.complex64)
+    from quantizationawarethzdoe_amd.optics import gaussian_beam
+    return gaussian_beam(N, N, dx, dx, [lam], [w], [w], device=device)
+
+
+def shard_planes(n_planes, rank, world):
+    """Contiguous block of plane indices of one rank (every plane exactly once)."""
+    base, extra = divmod(n_planes, world)
+    start = rank * base + min(rank, extra)
+    return list(range(start, start + base + (1 if rank < extra else 0)))
 
 
 def z_planes(rank, world):
+    """This rank's share of the global sweep (weak scaling: Z_PER_RANK planes per rank)."""
     total = Z_PER_RANK * world
     zs = torch.linspace(Z_MIN, Z_MAX, total, dtype=torch.float64)
-    return [float(v) for v in zs[rank * Z_PER_RANK:(rank + 1) * Z_PER_RANK]]
+    return [float(zs[i]) for i in shard_planes(total, rank, world)]
 
 
 def cpu_baseline(budget_s=12.0, max_planes=8):

@@ -193,6 +193,60 @@ int thz_radial_forward(const float* profile, int R, int H, int W, float* out, th
 int thz_radial_backward(const float* grad_out, int R, int H, int W, float* grad_profile, thz_stream_t stream);
 
 /*
+ * Optical elements around the DOE, generated / applied on the device.
+ *
+ * Guassian_beam.forward (LightSource/Gaussian_beam.py:88-160): out [1, C, H, W] complex64.
+ * waist_x / waist_y: host [C] fp32 beam waists (given, or BeamWaistCorruagtedTK :67-85).
+ */
+typedef struct thz_gauss_desc {
+  int C, H, W;
+  float dx, dy;                /* field spacing */
+  const float* wavelengths;    /* host [C] */
+  const float* waist_x;        /* host [C] */
+  const float* waist_y;        /* host [C] */
+  float x0, y0;                /* beam centre */
+  float z_w0x, z_w0y;          /* waist positions */
+  float alpha;                 /* amplitude rotation (rad) */
+} thz_gauss_desc;
+int thz_gaussian_beam(const thz_gauss_desc* d, void* out, thz_stream_t stream);
+
+/* Thin_LensElement.forward (Components/Thin_Lens.py:31-85): out = in * exp(-i pi r^2 / (lambda f)). */
+typedef struct thz_lens_desc {
+  int B, C, H, W;
+  float dx, dy, focal_length;
+  const float* wavelengths;    /* host [C] */
+} thz_lens_desc;
+int thz_thin_lens(const thz_lens_desc* d, const void* in, void* out, thz_stream_t stream);
+
+/* ApertureElement.forward (Components/Aperture.py:44-136): out = in * mask (in == out allowed). */
+#define THZ_APERTURE_RECT 1
+#define THZ_APERTURE_CIRC 2
+typedef struct thz_aperture_desc {
+  int BC, H, W, kind;
+  float dx, dy;
+  float half_w, half_h;        /* rect: open where |x| <= half_w and |y| <= half_h (fp32) */
+  float radius;                /* circ: open where sqrt(x^2 + y^2) <= radius */
+} thz_aperture_desc;
+int thz_aperture(const thz_aperture_desc* d, const void* in, void* out, thz_stream_t stream);
+
+/*
+ * QAT loss (experiment_four_focal_spots.ipynb:336-370): mean((normalize(|E|^2) - target)^2) with
+ * normalize dividing each batch item by its max (utils/Helper_Functions.py:185-193).
+ * target [tB, tC, H, W] broadcast over B / C (tB in {1, B}, tC in {1, C}).
+ * stats: device workspace of thz_intensity_mse_workspace_size bytes (max, argmax, max-path sum
+ * per batch item, kept for the backward); loss: device [1]; grad_loss: device [1].
+ */
+typedef struct thz_loss_desc {
+  int B, C, H, W;
+  int tB, tC;
+} thz_loss_desc;
+size_t thz_intensity_mse_workspace_size(const thz_loss_desc* d);
+int thz_intensity_mse_forward(const thz_loss_desc* d, const void* field, const float* target, float* loss,
+                              float* stats, thz_stream_t stream);
+int thz_intensity_mse_backward(const thz_loss_desc* d, const void* field, const float* target, const float* stats,
+                               const float* grad_loss, void* grad_field, thz_stream_t stream);
+
+/*
  * Batched 1-D FFT along the contiguous axis (the building block of ft2/ift2,
  * utils/Helper_Functions.py:150, without shifts): in/out [rows, n], unnormalised,
  * inverse != 0 for the backward transform.  n <= 16384, any factorisation.

@@ -397,6 +397,91 @@ def layer_height_map(cls, weight, lut, hmax, lam_min, eps, iter_frac, optim, num
     raise ValueError(f"unknown layer class {cls}")
 
 
+# ---------------------------------------------------------------------------------------------
+# optical elements and the QAT loss
+# ---------------------------------------------------------------------------------------------
+WAIST_FIT_E = [2.70171433587848e-13, 3.10350492358753e-10, -6.35088689290759e-07, 0.000322826804965868,
+               -0.0665921902050336, 6.08799187520401]
+WAIST_FIT_H = [-1.01507121315420e-11, 1.70791445624058e-08, -1.12281052414283e-05, 0.00360605624858374,
+               -0.564799749943028, 35.5588926870041]
+
+
+def waist_fit(wavelengths):
+    """BeamWaistCorruagtedTK (LightSource/Gaussian_beam.py:67-85) on f = c / lambda in GHz."""
+    f = (2.998e8 / wavelengths) / 1e9
+    return [1e-3 * (p[0] * f ** 5 + p[1] * f ** 4 + p[2] * f ** 3 + p[3] * f ** 2 + p[4] * f + p[5])
+            for p in (WAIST_FIT_E, WAIST_FIT_H)]
+
+
+def gaussian_beam(H, W, dx, dy, wavelengths, waist_x=None, waist_y=None, center=(0, 0), z_w0=(0, 0), alpha=0):
+    """Guassian_beam.forward (LightSource/Gaussian_beam.py:88-160) -> [1, C, H, W]."""
+    lam = torch.as_tensor(wavelengths).reshape(-1)
+    if waist_x is None:
+        wx0, wy0 = waist_fit(lam)
+    else:
+        wx0 = torch.full_like(lam, waist_x)
+        wy0 = torch.full_like(lam, waist_y)
+    dx, dy = torch.as_tensor(dx, dtype=lam.dtype), torch.as_tensor(dy, dtype=lam.dtype)
+    x = torch.linspace(-dx * H / 2, dx * H / 2, H, dtype=lam.dtype)
+    y = torch.linspace(-dy * W / 2, dy * W / 2, W, dtype=lam.dtype)
+    X, Y = torch.meshgrid(x, y, indexing="ij")
+    X, Y = X[None], Y[None]
+    lam3 = lam[:, None, None]
+    k = 2 * torch.pi / lam3
+    wx0, wy0 = wx0[:, None, None], wy0[:, None, None]
+    zx, zy = torch.tensor(z_w0[0], dtype=lam.dtype), torch.tensor(z_w0[1], dtype=lam.dtype)
+    x0, y0 = torch.tensor(center[0], dtype=lam.dtype), torch.tensor(center[1], dtype=lam.dtype)
+    a = torch.tensor(alpha, dtype=lam.dtype)
+    zrx, zry = torch.pi * wx0 ** 2 / lam3, torch.pi * wy0 ** 2 / lam3
+    gx, gy = torch.arctan2(zx, zrx), torch.arctan2(zy, zry)
+    wx = wx0 * torch.sqrt(1 + (zx / zrx) ** 2)
+    wy = wy0 * torch.sqrt(1 + (zy / zry) ** 2)
+    rx = 1e12 if z_w0[0] == 0 else zx * (1 + (zrx / zx) ** 2)
+    ry = 1e12 if z_w0[1] == 0 else zy * (1 + (zry / zy) ** 2)
+    xr = X * torch.cos(a) + Y * torch.sin(a)
+    yr = -X * torch.sin(a) + Y * torch.cos(a)
+    phase = torch.exp(-1j * ((k * zx + k * X ** 2 / (2 * rx) - gx) + (k * zy + k * Y ** 2 / (2 * ry) - gy)))
+    A = (wx0 / wx) * (wy0 / wy) * torch.exp(-(xr - x0) ** 2 / (wx ** 2) - (yr - y0) ** 2 / (wy ** 2))
+    return (A * phase)[None]
+
+
+def thin_lens(field, dx, dy, focal_length, wavelengths):
+    """Thin_LensElement.forward (Components/Thin_Lens.py:31-85)."""
+    H, W = field.shape[-2:]
+    lam = torch.as_tensor(wavelengths).reshape(-1)[:, None, None]
+    xc = torch.linspace(-((H - 1) // 2), (H - 1) // 2, H, dtype=lam.dtype)
+    yc = torch.linspace(-((W - 1) // 2), (W - 1) // 2, W, dtype=lam.dtype)
+    xg, yg = torch.meshgrid(xc, yc, indexing="ij")
+    xg = xg[None, None] * torch.tensor([dx], dtype=lam.dtype)[:, None, None]
+    yg = yg[None, None] * torch.tensor([dy], dtype=lam.dtype)[:, None, None]
+    f = torch.tensor([focal_length], dtype=lam.dtype)
+    ang = -(math.pi / (lam * f)) * (xg ** 2 + yg ** 2)
+    return field * torch.exp(1j * ang)
+
+
+def aperture_mask(H, W, dx, dy, kind, size):
+    """ApertureElement masks (Components/Aperture.py:61-118): rect on an 'xy' grid, circ on 'ij'."""
+    dx, dy = torch.as_tensor(dx, dtype=torch.float32), torch.as_tensor(dy, dtype=torch.float32)
+    if kind == "rect":
+        rw = min(size, dx * W) if size is not None else dx * W / 2
+        rh = min(size, dy * H) if size is not None else dy * H / 2
+        x = torch.linspace(-dx * W / 2, dx * W / 2, W, dtype=dx.dtype)
+        y = torch.linspace(-dy * H / 2, dy * H / 2, H, dtype=dy.dtype)
+        X, Y = torch.meshgrid(x, y, indexing="xy")
+        return torch.where((torch.abs(X) <= rw / 2) & (torch.abs(Y) <= rh / 2), 1, 0)
+    r = torch.tensor(size)
+    x = torch.linspace(-dx * H / 2, dx * H / 2, H, dtype=dx.dtype)
+    y = torch.linspace(-dy * W / 2, dy * W / 2, W, dtype=dy.dtype)
+    X, Y = torch.meshgrid(x, y, indexing="ij")
+    return torch.where(torch.sqrt(X ** 2 + Y ** 2) <= r, 1, 0)
+
+
+def intensity_mse(field, target):
+    """MSE(normalize(|E|^2), target) of the QAT loop (experiment_four_focal_spots.ipynb:336-370)."""
+    amp = normalize(torch.abs(field) ** 2)
+    return torch.mean((amp - target.expand_as(amp)) ** 2)
+
+
 def normalize(x):
     """Per-batch divide by max (utils/Helper_Functions.py:185-193), out of place."""
     B = x.shape[0]

@@ -31,6 +31,8 @@ EXPORTED = [
     "thz_rsc_workspace_size", "thz_rsc_forward",
     "thz_doe_modulate_forward", "thz_doe_modulate_backward", "thz_quant_forward", "thz_quant_backward",
     "thz_radial_forward", "thz_radial_backward",
+    "thz_gaussian_beam", "thz_thin_lens", "thz_aperture",
+    "thz_intensity_mse_workspace_size", "thz_intensity_mse_forward", "thz_intensity_mse_backward",
     "thz_fft_rows",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
@@ -91,6 +93,40 @@ class QuantDesc(ctypes.Structure):
     ]
 
 
+class GaussDesc(ctypes.Structure):
+    _fields_ = [
+        ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("dx", ctypes.c_float), ("dy", ctypes.c_float),
+        ("wavelengths", ctypes.POINTER(ctypes.c_float)), ("waist_x", ctypes.POINTER(ctypes.c_float)),
+        ("waist_y", ctypes.POINTER(ctypes.c_float)),
+        ("x0", ctypes.c_float), ("y0", ctypes.c_float), ("z_w0x", ctypes.c_float), ("z_w0y", ctypes.c_float),
+        ("alpha", ctypes.c_float),
+    ]
+
+
+class LensDesc(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("focal_length", ctypes.c_float),
+        ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+    ]
+
+
+class ApertureDesc(ctypes.Structure):
+    _fields_ = [
+        ("BC", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int), ("kind", ctypes.c_int),
+        ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("half_w", ctypes.c_float), ("half_h", ctypes.c_float),
+        ("radius", ctypes.c_float),
+    ]
+
+
+class LossDesc(ctypes.Structure):
+    _fields_ = [("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+                ("tB", ctypes.c_int), ("tC", ctypes.c_int)]
+
+
+APERTURE_RECT, APERTURE_CIRC = 1, 2
+
 Q_FP, Q_STE, Q_PSQ, Q_SGV3, Q_NGS, Q_SGV1 = 0, 1, 2, 3, 4, 5
 THZ_MAX_LUT = 16
 
@@ -118,11 +154,20 @@ def _declare(lib):
     lib.thz_radial_backward.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]
     lib.thz_czt_workspace_size.argtypes = [ctypes.POINTER(CztDesc), ctypes.POINTER(c_size_t)]
     lib.thz_czt_forward.argtypes = [ctypes.POINTER(CztDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.thz_gaussian_beam.argtypes = [ctypes.POINTER(GaussDesc), c_void_p, c_void_p]
+    lib.thz_thin_lens.argtypes = [ctypes.POINTER(LensDesc), c_void_p, c_void_p, c_void_p]
+    lib.thz_aperture.argtypes = [ctypes.POINTER(ApertureDesc), c_void_p, c_void_p, c_void_p]
+    lib.thz_intensity_mse_workspace_size.argtypes = [ctypes.POINTER(LossDesc)]
+    lib.thz_intensity_mse_forward.argtypes = [ctypes.POINTER(LossDesc), c_void_p, c_void_p, c_void_p, c_void_p,
+                                              c_void_p]
+    lib.thz_intensity_mse_backward.argtypes = [ctypes.POINTER(LossDesc), c_void_p, c_void_p, c_void_p, c_void_p,
+                                               c_void_p, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]
     lib.thz_timing_reset.argtypes = []
     lib.thz_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
     for name in EXPORTED[2:]:
         getattr(lib, name).restype = c_int
+    lib.thz_intensity_mse_workspace_size.restype = c_size_t
 
 
 def lib():

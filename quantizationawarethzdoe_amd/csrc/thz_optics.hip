@@ -1,0 +1,359 @@
+// Optical elements around the DOE and the QAT loss, for gfx950.
+//
+//  * Gaussian source   LightSource/Gaussian_beam.py:88-160  E = A(x, y) exp(-i phi(x, y)); the
+//                      per-wavelength scalars (waist, Rayleigh range, Gouy phase, spot size,
+//                      curvature) are fp32 host values in the reference's op order, the per-pixel
+//                      part runs here (no host-built grid, no H2D copy).
+//  * thin lens         Components/Thin_Lens.py:31-58    field * exp(i ang), ang = -(pi/(lambda f)) r^2
+//  * aperture          Components/Aperture.py:44-136    field * mask (rect: 'xy' grid, circ: 'ij')
+//  * |E|^2 -> normalize -> MSE   utils/Helper_Functions.py:185-193 + nn.MSELoss
+//                      (experiment_four_focal_spots.ipynb:336-370): one workgroup per batch item
+//                      finds max / argmax of |E|^2, the squared error and the sum the backward's
+//                      max-path needs; the backward is then one elementwise pass.
+#include <cmath>
+
+#include "thz_common.hpp"
+#include "thz_dev.hpp"
+
+#pragma clang fp contract(off)
+
+namespace thz {
+
+struct GaussArgs {
+  int C, H, W;
+  float x_start, x_end, y_start, y_end;
+  float x0, y0, ca, sa;
+  float k[THZ_MAX_WAVELENGTHS], kz_x[THZ_MAX_WAVELENGTHS], kz_y[THZ_MAX_WAVELENGTHS];
+  float two_rx[THZ_MAX_WAVELENGTHS], two_ry[THZ_MAX_WAVELENGTHS];
+  float gouy_x[THZ_MAX_WAVELENGTHS], gouy_y[THZ_MAX_WAVELENGTHS];
+  float amp[THZ_MAX_WAVELENGTHS], wx2[THZ_MAX_WAVELENGTHS], wy2[THZ_MAX_WAVELENGTHS];
+};
+
+__global__ void gaussian_beam_kernel(float2* __restrict__ out, GaussArgs a) {
+  const int HW = a.H * a.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  const int i = p / a.W, j = p - i * a.W;
+  const float X = lin(a.x_start, a.x_end, a.H, i);  // meshgrid 'ij': X follows the height axis
+  const float Y = lin(a.y_start, a.y_end, a.W, j);
+  const float xr = X * a.ca + Y * a.sa;
+  const float yr = -X * a.sa + Y * a.ca;
+  const float dx = xr - a.x0, dy = yr - a.y0;
+  for (int c = 0; c < a.C; ++c) {
+    const float ph = ((a.kz_x[c] + (a.k[c] * (X * X)) / a.two_rx[c]) - a.gouy_x[c]) +
+                     ((a.kz_y[c] + (a.k[c] * (Y * Y)) / a.two_ry[c]) - a.gouy_y[c]);
+    const float A = a.amp[c] * expf(-(dx * dx) / a.wx2[c] - (dy * dy) / a.wy2[c]);
+    float sn, cs;
+    sincos_rad(ph, &sn, &cs);
+    out[(size_t)c * HW + p] = make_float2(A * cs, -(A * sn));  // A exp(-i ph)
+  }
+}
+
+struct LensArgs {
+  int B, C, H, W;
+  float gx0, gx1, gy0, gy1;  // linspace(-((n-1)//2), (n-1)//2, n) end points
+  float dx, dy;
+  float coef[THZ_MAX_WAVELENGTHS];  // pi / (lambda f), fp32
+};
+
+__global__ void thin_lens_kernel(const float2* __restrict__ in, float2* __restrict__ out, LensArgs a) {
+  const int HW = a.H * a.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  const int i = p / a.W, j = p - i * a.W;
+  const float xg = lin(a.gx0, a.gx1, a.H, i) * a.dx;
+  const float yg = lin(a.gy0, a.gy1, a.W, j) * a.dy;
+  const float r2 = xg * xg + yg * yg;
+  for (int c = 0; c < a.C; ++c) {
+    const float ang = -a.coef[c] * r2;
+    float sn, cs;
+    sincos_rad(ang, &sn, &cs);
+    for (int b = 0; b < a.B; ++b) {
+      const size_t idx = ((size_t)b * a.C + c) * HW + p;
+      out[idx] = cmul(in[idx], make_float2(cs, sn));
+    }
+  }
+}
+
+struct ApertureArgs {
+  int BC, H, W, kind;  // THZ_APERTURE_*
+  float ax0, ax1, ay0, ay1;  // linspace end points of the two grid axes
+  float half_w, half_h, radius;
+};
+
+__device__ __forceinline__ bool aperture_open(const ApertureArgs& a, int i, int j) {
+  if (a.kind == THZ_APERTURE_RECT) {
+    // meshgrid(x over W, y over H, indexing='xy'): X[i, j] = x[j], Y[i, j] = y[i]
+    const float X = lin(a.ax0, a.ax1, a.W, j), Y = lin(a.ay0, a.ay1, a.H, i);
+    return fabsf(X) <= a.half_w && fabsf(Y) <= a.half_h;
+  }
+  // circ: meshgrid(x over H, y over W) 'ij'
+  const float X = lin(a.ax0, a.ax1, a.H, i), Y = lin(a.ay0, a.ay1, a.W, j);
+  return sqrtf(X * X + Y * Y) <= a.radius;
+}
+
+__global__ void aperture_kernel(const float2* __restrict__ in, float2* __restrict__ out, ApertureArgs a) {
+  const int HW = a.H * a.W;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HW) return;
+  const bool open = aperture_open(a, p / a.W, p % a.W);
+  for (int bc = 0; bc < a.BC; ++bc) {
+    const size_t idx = (size_t)bc * HW + p;
+    out[idx] = open ? in[idx] : make_float2(0.f * in[idx].x, 0.f * in[idx].y);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// |E|^2 -> normalize (per batch item, by its max) -> MSE against a broadcast target
+// stats[b] = {max, argmax (as float bits), sum_i r_i I_i} with r_i = I_i/m - T_i
+// ---------------------------------------------------------------------------------------------
+constexpr int LOSS_THREADS = 1024;
+
+struct LossArgs {
+  int B, C, H, W, tB, tC;
+};
+
+__device__ __forceinline__ float target_at(const float* t, const LossArgs& a, int b, int c, int p) {
+  const int tb = a.tB == 1 ? 0 : b, tc = a.tC == 1 ? 0 : c;
+  return t[((size_t)tb * a.tC + tc) * a.H * a.W + p];
+}
+
+__device__ __forceinline__ float intensity(float2 e) {
+  // torch.abs(E) ** 2: |E| = hypot, then squared
+  const float m = hypotf(e.x, e.y);
+  return m * m;
+}
+
+__global__ void __launch_bounds__(LOSS_THREADS) mse_forward_kernel(const float2* __restrict__ f,
+                                                                   const float* __restrict__ t,
+                                                                   float* __restrict__ partial,
+                                                                   float* __restrict__ stats, LossArgs a) {
+  __shared__ float s_v[LOSS_THREADS / 64];
+  __shared__ int s_i[LOSS_THREADS / 64];
+  __shared__ float s_a[LOSS_THREADS / 64], s_b[LOSS_THREADS / 64];
+  const int b = blockIdx.x;
+  const int HW = a.H * a.W, n = a.C * HW;
+  const float2* fb = f + (size_t)b * n;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // pass 1: max and its first index
+  float mv = -1.f;
+  int mi = 0x7fffffff;
+  for (int i = threadIdx.x; i < n; i += LOSS_THREADS) {
+    const float v = intensity(fb[i]);
+    if (v > mv) { mv = v; mi = i; }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(mv, o);
+    const int oi = __shfl_xor(mi, o);
+    if (ov > mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
+  }
+  if (lane == 0) { s_v[wid] = mv; s_i[wid] = mi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < LOSS_THREADS / 64; ++w)
+      if (s_v[w] > s_v[0] || (s_v[w] == s_v[0] && s_i[w] < s_i[0])) { s_v[0] = s_v[w]; s_i[0] = s_i[w]; }
+  }
+  __syncthreads();
+  const float m = s_v[0];
+  // pass 2: sum (I/m - T)^2 and sum (I/m - T) I
+  float se = 0.f, sr = 0.f;
+  for (int i = threadIdx.x; i < n; i += LOSS_THREADS) {
+    const int c = i / HW, p = i - c * HW;
+    const float I = intensity(fb[i]);
+    const float r = I / m - target_at(t, a, b, c, p);
+    se += r * r;
+    sr += r * I;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    se += __shfl_xor(se, o);
+    sr += __shfl_xor(sr, o);
+  }
+  if (lane == 0) { s_a[wid] = se; s_b[wid] = sr; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float A = 0.f, Bv = 0.f;
+    for (int w = 0; w < LOSS_THREADS / 64; ++w) { A += s_a[w]; Bv += s_b[w]; }
+    partial[b] = A;
+    stats[3 * b + 0] = m;
+    stats[3 * b + 1] = __int_as_float(s_i[0]);
+    stats[3 * b + 2] = Bv;
+  }
+}
+
+__global__ void mse_finish_kernel(const float* __restrict__ partial, float* __restrict__ loss, int B, float inv_n) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += partial[b];
+    loss[0] = s * inv_n;
+  }
+}
+
+// dL/dE = 2 E dL/dI;  dL/dI_j = g (r_j / m - [j == argmax] sum_i r_i I_i / m^2),  g = 2 grad / N
+__global__ void mse_backward_kernel(const float2* __restrict__ f, const float* __restrict__ t,
+                                    const float* __restrict__ stats, const float* __restrict__ grad_loss,
+                                    float2* __restrict__ gf, LossArgs a, float two_inv_n) {
+  const int HW = a.H * a.W, n = a.C * HW;
+  const size_t total = (size_t)a.B * n;
+  const size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= total) return;
+  const int b = (int)(q / n), i = (int)(q - (size_t)b * n);
+  const int c = i / HW, p = i - c * HW;
+  const float m = stats[3 * b], S = stats[3 * b + 2];
+  const int am = __float_as_int(stats[3 * b + 1]);
+  const float g = grad_loss[0] * two_inv_n;
+  const float2 e = f[q];
+  const float I = intensity(e);
+  const float r = I / m - target_at(t, a, b, c, p);
+  float dI = g * r / m;
+  if (i == am) dI -= g * S / (m * m);
+  gf[q] = make_float2(2.f * dI * e.x, 2.f * dI * e.y);
+}
+
+static bool loss_args(const thz_loss_desc* d, LossArgs* a) {
+  if (!d || d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1) return false;
+  if (!(d->tB == 1 || d->tB == d->B) || !(d->tC == 1 || d->tC == d->C)) return false;
+  *a = LossArgs{d->B, d->C, d->H, d->W, d->tB, d->tC};
+  return true;
+}
+
+}  // namespace thz
+
+using namespace thz;
+
+extern "C" int thz_gaussian_beam(const thz_gauss_desc* d, void* out, thz_stream_t stream) {
+  if (!d || !out || d->C < 1 || d->H < 1 || d->W < 1 || !d->wavelengths || !d->waist_x || !d->waist_y)
+    return fail(THZ_E_ARG, "bad Gaussian-beam arguments");
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  GaussArgs a{};
+  a.C = d->C;
+  a.H = d->H;
+  a.W = d->W;
+  // x = linspace(-dx H / 2, dx H / 2, H) (:92-97), all fp32 as the reference's tensors
+  a.x_start = (-d->dx * (float)d->H) / 2.0f;
+  a.x_end = (d->dx * (float)d->H) / 2.0f;
+  a.y_start = (-d->dy * (float)d->W) / 2.0f;
+  a.y_end = (d->dy * (float)d->W) / 2.0f;
+  a.x0 = d->x0;
+  a.y0 = d->y0;
+  a.ca = std::cos(d->alpha);
+  a.sa = std::sin(d->alpha);
+  const float PI = 3.14159265358979323846f, TWO_PI = 6.28318530717958647692f;
+  for (int c = 0; c < d->C; ++c) {
+    const float lam = d->wavelengths[c], w0x = d->waist_x[c], w0y = d->waist_y[c];
+    const float k = TWO_PI / lam;
+    const float zrx = (PI * (w0x * w0x)) / lam, zry = (PI * (w0y * w0y)) / lam;  // Rayleigh (:126-127)
+    const float gx = std::atan2(d->z_w0x, zrx), gy = std::atan2(d->z_w0y, zry);   // Gouy (:130-131)
+    const float qx = d->z_w0x / zrx, qy = d->z_w0y / zry;
+    const float wx = w0x * std::sqrt(1.0f + qx * qx), wy = w0y * std::sqrt(1.0f + qy * qy);
+    float rx = 1e12f, ry = 1e12f;  // curvature (:138-145); 1e12 at the waist
+    if (d->z_w0x != 0.0f) { const float t = zrx / d->z_w0x; rx = d->z_w0x * (1.0f + t * t); }
+    if (d->z_w0y != 0.0f) { const float t = zry / d->z_w0y; ry = d->z_w0y * (1.0f + t * t); }
+    a.k[c] = k;
+    a.kz_x[c] = k * d->z_w0x;
+    a.kz_y[c] = k * d->z_w0y;
+    a.two_rx[c] = 2.0f * rx;
+    a.two_ry[c] = 2.0f * ry;
+    a.gouy_x[c] = gx;
+    a.gouy_y[c] = gy;
+    a.amp[c] = (w0x / wx) * (w0y / wy);
+    a.wx2[c] = wx * wx;
+    a.wy2[c] = wy * wy;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("gaussian_beam", s);
+  const int n = d->H * d->W;
+  hipLaunchKernelGGL(gaussian_beam_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (float2*)out, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_thin_lens(const thz_lens_desc* d, const void* in, void* out, thz_stream_t stream) {
+  if (!d || !in || !out || d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1 || !d->wavelengths)
+    return fail(THZ_E_ARG, "bad thin-lens arguments");
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  LensArgs a{};
+  a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W;
+  a.gx0 = (float)(-((d->H - 1) / 2));
+  a.gx1 = (float)((d->H - 1) / 2);
+  a.gy0 = (float)(-((d->W - 1) / 2));
+  a.gy1 = (float)((d->W - 1) / 2);
+  a.dx = d->dx;
+  a.dy = d->dy;
+  const float PI = 3.14159265358979323846f;
+  for (int c = 0; c < d->C; ++c) a.coef[c] = PI / (d->wavelengths[c] * d->focal_length);
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("thin_lens", s);
+  const int n = d->H * d->W;
+  hipLaunchKernelGGL(thin_lens_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_aperture(const thz_aperture_desc* d, const void* in, void* out, thz_stream_t stream) {
+  if (!d || !in || !out || d->BC < 1 || d->H < 1 || d->W < 1) return fail(THZ_E_ARG, "bad aperture arguments");
+  if (d->kind != THZ_APERTURE_RECT && d->kind != THZ_APERTURE_CIRC)
+    return fail(THZ_E_ARG, "bad aperture kind %d", d->kind);
+  ApertureArgs a{};
+  a.BC = d->BC; a.H = d->H; a.W = d->W; a.kind = d->kind;
+  if (d->kind == THZ_APERTURE_RECT) {
+    a.ax0 = (-d->dx * (float)d->W) / 2.0f;  // x over W with dx (Aperture.py:115)
+    a.ax1 = (d->dx * (float)d->W) / 2.0f;
+    a.ay0 = (-d->dy * (float)d->H) / 2.0f;  // y over H with dy (:116)
+    a.ay1 = (d->dy * (float)d->H) / 2.0f;
+  } else {
+    a.ax0 = (-d->dx * (float)d->H) / 2.0f;  // x over H with dx (:76)
+    a.ax1 = (d->dx * (float)d->H) / 2.0f;
+    a.ay0 = (-d->dy * (float)d->W) / 2.0f;
+    a.ay1 = (d->dy * (float)d->W) / 2.0f;
+  }
+  a.half_w = d->half_w;
+  a.half_h = d->half_h;
+  a.radius = d->radius;
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("aperture", s);
+  const int n = d->H * d->W;
+  hipLaunchKernelGGL(aperture_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" size_t thz_intensity_mse_workspace_size(const thz_loss_desc* d) {
+  return d && d->B > 0 ? sizeof(float) * 4 * (size_t)d->B : 0;
+}
+
+extern "C" int thz_intensity_mse_forward(const thz_loss_desc* d, const void* field, const float* target, float* loss,
+                                         float* stats, thz_stream_t stream) {
+  LossArgs a;
+  if (!loss_args(d, &a) || !field || !target || !loss || !stats) return fail(THZ_E_ARG, "bad loss arguments");
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("intensity_mse_fwd", s);
+  float* partial = stats + 3 * (size_t)d->B;
+  hipLaunchKernelGGL(mse_forward_kernel, dim3(d->B), dim3(LOSS_THREADS), 0, s, (const float2*)field, target, partial,
+                     stats, a);
+  THZ_LAUNCH_CHECK();
+  const double n = (double)d->B * d->C * d->H * d->W;
+  hipLaunchKernelGGL(mse_finish_kernel, dim3(1), dim3(64), 0, s, partial, loss, d->B, (float)(1.0 / n));
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_intensity_mse_backward(const thz_loss_desc* d, const void* field, const float* target,
+                                          const float* stats, const float* grad_loss, void* grad_field,
+                                          thz_stream_t stream) {
+  LossArgs a;
+  if (!loss_args(d, &a) || !field || !target || !stats || !grad_loss || !grad_field)
+    return fail(THZ_E_ARG, "bad loss arguments");
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("intensity_mse_bwd", s);
+  const size_t total = (size_t)d->B * d->C * d->H * d->W;
+  const double n = (double)total;
+  hipLaunchKernelGGL(mse_backward_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s,
+                     (const float2*)field, target, stats, grad_loss, (float2*)grad_field, a, (float)(2.0 / n));
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}

@@ -1,0 +1,176 @@
+"""Quantization-aware training loop of the four-focal-spots DOE (cfg4) and its data-parallel form.
+
+The system is the reference notebook's (experiment_four_focal_spots.ipynb, cells 1-6):
+Gaussian source (BeamWaistCorruagtedTK waist) -> ASM 127 mm (padding 2, exact band limit)
+-> thin lens f = 127 mm -> 80 mm square aperture -> score-Gumbel DOE (v3) -> ASM 200 mm ->
+loss = MSE(normalize(|E|^2), nine-spot target), Adam lr 0.02, iter_frac = itr / max_itrs.
+
+MI355X mapping
+  * every stage is a HIP kernel of libthzdoe (source, lens and aperture once at construction;
+    per step: fused quantizer, fused modulate, the 3-pass ASM and its adjoint, the fused
+    |E|^2 -> normalize -> MSE forward/backward);
+  * data parallel: the DOE weight is replicated, each rank evaluates the
+    loss on its own noise sample (Gumbel + fabrication tolerance, generator seeded
+    base + rank) and the weight gradients are averaged by ONE flat all-reduce (RCCL over
+    xGMI on the GPU, gloo in the CPU tests) before the optimiser step -- an N-sample
+    estimator per step.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+
+from quantizationawarethzdoe_amd import optics as _optics
+from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
+from quantizationawarethzdoe_amd.Components.Thin_Lens import Thin_LensElement
+from quantizationawarethzdoe_amd.LightSource.Gaussian_beam import Guassian_beam
+from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+from quantizationawarethzdoe_amd.utils.Helper_Functions import normalize
+from quantizationawarethzdoe_amd.utils.units import m, mm, um
+
+C0 = 2.998e8
+FOCI_MM = [(-20, -20), (20, 20), (-20, 20), (20, -20), (0, 0), (0, -20), (-20, 0), (0, 20), (20, 0)]
+
+
+def default_params():
+    """doe_params / optim_params of the notebook (cell 1)."""
+    doe_params = {
+        'doe_size': [100, 100], 'doe_dxy': 1 * mm, 'doe_level': 4, 'look_up_table': None, 'num_unit': 2,
+        'height_constraint_max': 1 * mm, 'tolerance': 10 * um, 'material': [2.66, 0.03],
+    }
+    optim_params = {'c_s': 100, 'tau_max': 2.5, 'tau_min': 1.5}
+    return doe_params, optim_params
+
+
+def define_FoM(resolution, sampling_size, wavelength, focal_length, position, device=None):
+    """Gaussian PSF with the diffraction-limited FWHM at ``position`` (notebook cell 2), max 1."""
+    device = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    height, width = resolution
+    Lx, Ly = sampling_size * width, sampling_size * height
+    eff_L = torch.sqrt(torch.tensor(Lx ** 2 + Ly ** 2, device=device))
+    NA = torch.sin(torch.atan(eff_L / (2 * focal_length)))
+    fwhm = wavelength / (2 * NA)
+    xg, yg = torch.meshgrid(torch.linspace(-Lx / 2, Lx / 2, steps=width, device=device),
+                            torch.linspace(-Ly / 2, Ly / 2, steps=height, device=device), indexing="ij")
+    x0, y0 = torch.tensor(position, device=device)
+    psf = torch.exp(-((xg - x0) ** 2 + (yg - y0) ** 2) / ((fwhm * 2) ** 2))
+    return normalize(psf.unsqueeze(0).unsqueeze(0))
+
+
+def four_focal_spots_target(wavelength=C0 / 300e9, resolution=(100, 100), dxy=1 * mm, device=None):
+    """Sum of the nine PSFs of notebook cell 3 ([1, 1, H, W])."""
+    return sum(define_FoM(list(resolution), dxy, wavelength, 200 * mm, [a * mm, b * mm], device=device)
+               for a, b in FOCI_MM)
+
+
+class FourFocalSpotsSystem(nn.Module):
+    """Submm_Setupv2 of the notebook (cell 4): fixed optics before the DOE, DOE, ASM to the target."""
+
+    def __init__(self, input_dxy=1 * mm, input_field_shape=(100, 100), doe_params=None, optim_params=None,
+                 wavelengths=C0 / 300e9, doe_class=Q.SoftGumbelQuantizedDOELayerv3, device=None):
+        super().__init__()
+        dp, op = default_params()
+        self.doe_params = doe_params or dp
+        self.optim_params = optim_params or op
+        self.device = device or torch.device("cuda")
+        self.wavelengths = wavelengths
+        self.source = Guassian_beam(height=input_field_shape[0], width=input_field_shape[1], beam_waist_x=None,
+                                    beam_waist_y=None, wavelengths=wavelengths, spacing=input_dxy, device=self.device)
+        self.asm_prop1 = ASM_prop(z_distance=0.127 * m, bandlimit_type='exact', padding_scale=2,
+                                  bandlimit_kernel=True, device=self.device)
+        self.Colli_lens = Thin_LensElement(focal_length=0.127 * m)
+        self.aperture = ApertureElement(aperture_type='rect', aperture_size=0.08)
+        with torch.no_grad():
+            self.input_field = self.field_before_DOE()
+        if doe_class.__name__.endswith("FullPrecisionDOELayer"):
+            self.doe = doe_class(self.doe_params, device=self.device)
+        else:
+            self.doe = doe_class(self.doe_params, self.optim_params, device=self.device)
+        self.asm_prop3 = ASM_prop(z_distance=200 * mm, bandlimit_type='exact', padding_scale=2,
+                                  bandlimit_kernel=True, device=self.device)
+
+    def field_before_DOE(self):
+        field = self.source()
+        field = self.asm_prop1(field)
+        field = self.Colli_lens(field)
+        return self.aperture(field)
+
+    def forward(self, iter_frac):
+        return self.asm_prop3(self.doe(self.input_field, iter_frac))
+
+
+class GradientAllReduce:
+    """Average the gradients of ``params`` over the process group with ONE flat all-reduce.
+
+    10 KB for cfg4 (50 x 50 fp32): latency-bound, so a single bucket; the flat buffer is
+    allocated once and reused every step.
+    """
+
+    def __init__(self, params, group=None):
+        self.params = [p for p in params if p.requires_grad]
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        n = sum(p.numel() for p in self.params)
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
+
+    def __call__(self):
+        if self.world == 1:
+            return
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            if p.grad is None:
+                self.flat[off:off + k].zero_()
+            else:
+                self.flat[off:off + k].copy_(p.grad.reshape(-1))
+            off += k
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        self.flat.mul_(1.0 / self.world)
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            g = self.flat[off:off + k].view_as(p)
+            if p.grad is None:
+                p.grad = g.clone()
+            else:
+                p.grad.copy_(g)
+            off += k
+
+
+class QATTrainer:
+    """One QAT iteration = forward, fused loss, backward, gradient all-reduce, Adam step."""
+
+    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None):
+        self.system = system
+        self.target = target.to(system.device).float().contiguous()
+        self.max_itrs = max_itrs
+        self.optimizer = torch.optim.Adam(system.parameters(), lr=lr)
+        self.allreduce = GradientAllReduce(list(system.parameters()), group=group)
+        self.itr = 0
+
+    def step(self, iter_frac=None):
+        frac = self.itr / self.max_itrs if iter_frac is None else iter_frac
+        out = self.system(frac)
+        loss = _optics.intensity_mse(out.data, self.target)
+        self.optimizer.zero_grad(set_to_none=False)
+        loss.backward()
+        self.allreduce()
+        self.optimizer.step()
+        self.itr += 1
+        return loss
+
+    def train(self, steps, log_every=200, log=print):
+        t0 = time.perf_counter()
+        losses = []
+        for _ in range(steps):
+            loss = self.step()
+            losses.append(loss.detach())
+            if log_every and (self.itr - 1) % log_every == 0:
+                log(f"The iteration : {self.itr - 1}, Loss: {float(loss):.6g}")
+        torch.cuda.synchronize()
+        return torch.stack(losses).cpu(), time.perf_counter() - t0

@@ -62,4 +62,5 @@ def import_reference():
     ns.DOE = importlib.import_module("Components.QuantizedDOE")
     ns.GB = importlib.import_module("LightSource.Gaussian_beam")
     ns.HF = importlib.import_module("utils.Helper_Functions")
+    ns.import_module = importlib.import_module
     return ns

@@ -402,13 +402,137 @@ def gen_doe_layers(manifest):
     np.savez_compressed(os.path.join(HERE, "doe_layers_golden.npz"), **arrays)
 
 
+def gen_optics(manifest):
+    """Gaussian source, thin lens, aperture and the normalize+MSE loss of the QAT loop."""
+    arrays = {}
+    manifest["optics"] = []
+    G = ref.import_module("LightSource.Gaussian_beam")
+    TL = ref.import_module("Components.Thin_Lens")
+    AP = ref.import_module("Components.Aperture")
+    HF = ref.import_module("utils.Helper_Functions")
+    gauss_cases = [
+        ("gauss_tk", dict(height=100, width=100, beam_waist_x=None, beam_waist_y=None), [300], 1.0),
+        ("gauss_full", dict(height=64, width=80, beam_waist_x=6 * MM, beam_waist_y=4 * MM, center=(5 * MM, -3 * MM),
+                            z_w0=(10 * MM, 20 * MM), alpha=0.3), [280, 320], 0.5),
+        ("gauss_tk2", dict(height=48, width=48, beam_waist_x=None, beam_waist_y=None), [240, 300, 330], 1.0),
+    ]
+    for name, kw, freqs, dmm in gauss_cases:
+        wl = [C0 / (g * 1e9) for g in freqs]
+        src = G.Guassian_beam(wavelengths=wl_arg(wl), spacing=dmm * MM, device="cpu", **kw)
+        E = src()
+        arrays[f"{name}__out32"] = E.data.detach().numpy()
+        manifest["optics"].append(dict(name=name, kind="gauss", kw={k: v for k, v in kw.items()}, f=freqs,
+                                       dxy=dmm * MM))
+    x = rand_field((2, 2, 64, 80), 41)
+    arrays["field_in"] = x
+    g = rand_field((2, 2, 64, 80), 42)
+    arrays["field_gout"] = g
+    for name, kind, arg in [("lens_f127", "lens", 0.127), ("lens_f50", "lens", 0.05),
+                            ("rect_30", "rect", 0.03), ("rect_big", "rect", 0.5), ("circ_12", "circ", 0.012)]:
+        field = make_field(x, wl_arg([C0 / 280e9, C0 / 320e9]), [0.5 * MM, 0.7 * MM], False)
+        field._data = field._data.clone().requires_grad_(True)
+        if kind == "lens":
+            el = TL.Thin_LensElement(focal_length=arg)
+        else:
+            el = AP.ApertureElement(aperture_type=kind, aperture_size=arg)
+        out = el(field)
+        gx, = torch.autograd.grad(out.data, field._data, grad_outputs=torch.from_numpy(g))
+        arrays[f"{name}__out32"] = out.data.detach().numpy()
+        arrays[f"{name}__gx32"] = gx.numpy()
+        manifest["optics"].append(dict(name=name, kind=kind, arg=arg, f=[280, 320], dx=0.5 * MM, dy=0.7 * MM))
+    # loss: MSE(normalize(|E|^2), target) with the target broadcast over batch and channel
+    xl = rand_field((3, 2, 32, 32), 43)
+    tgt = np.random.default_rng(44).random((1, 1, 32, 32)).astype(np.float32)
+    E = torch.from_numpy(xl).requires_grad_(True)
+    amp = HF.normalize(torch.abs(E) ** 2)
+    loss = torch.nn.MSELoss()(amp, torch.from_numpy(tgt).expand(3, 2, 32, 32))
+    gE, = torch.autograd.grad(loss, E)
+    arrays.update({"loss_in": xl, "loss_target": tgt, "loss_value": np.float32(loss.item()),
+                   "loss_grad": gE.numpy()})
+    np.savez_compressed(os.path.join(HERE, "optics_golden.npz"), **arrays)
+    print("optics", len(manifest["optics"]))
+
+
+def _fom(resolution, dxy, wavelength, focal_length, position):
+    """The notebook's define_FoM PSF (experiment_four_focal_spots.ipynb cell 2), restated."""
+    HF = ref.HF
+    h, w = resolution
+    Lx, Ly = dxy * w, dxy * h
+    effL = torch.sqrt(torch.tensor(Lx ** 2 + Ly ** 2))
+    NA = torch.sin(torch.atan(effL / (2 * focal_length)))
+    fwhm = wavelength / (2 * NA)
+    xg, yg = torch.meshgrid(torch.linspace(-Lx / 2, Lx / 2, steps=w), torch.linspace(-Ly / 2, Ly / 2, steps=h))
+    x0, y0 = torch.tensor(position)
+    psf = torch.exp(-((xg - x0) ** 2 + (yg - y0) ** 2) / ((fwhm * 2) ** 2))
+    return HF.normalize(psf.unsqueeze(0).unsqueeze(0))
+
+
+FOCI = [(-20, -20), (20, 20), (-20, 20), (20, -20), (0, 0), (0, -20), (-20, 0), (0, 20), (20, 0)]
+
+
+def gen_qat(manifest, steps=20):
+    """cfg4: the four-focal-spots QAT system (notebook cells 1-6) on CPU, a seeded trace of
+    `steps` Adam steps with every RNG draw recorded."""
+    G = ref.import_module("LightSource.Gaussian_beam")
+    TL = ref.import_module("Components.Thin_Lens")
+    AP = ref.import_module("Components.Aperture")
+    HF = ref.HF
+    wl = C0 / 300e9
+    doe_params = dict(doe_size=[100, 100], doe_dxy=1 * MM, doe_level=4, look_up_table=None, num_unit=2,
+                      height_constraint_max=1 * MM, tolerance=10e-6, material=[2.66, 0.03])
+    optim_params = dict(c_s=100, tau_max=2.5, tau_min=1.5)
+    target = sum(_fom([100, 100], 1 * MM, wl, 200 * MM, [a * MM, b * MM]) for a, b in FOCI)
+    src = G.Guassian_beam(height=100, width=100, beam_waist_x=None, beam_waist_y=None, wavelengths=wl,
+                          spacing=1 * MM, device="cpu")
+    asm1 = ref.ASM.ASM_prop(z_distance=0.127, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True,
+                            device="cpu")
+    lens = TL.Thin_LensElement(focal_length=0.127)
+    ap = AP.ApertureElement(aperture_type='rect', aperture_size=0.08)
+    f0, _ = quiet(src)
+    f1, _ = quiet(asm1, f0)
+    f2 = lens(f1)
+    field_in = ap(f2)
+    torch.manual_seed(2024)
+    doe = ref.DOE.SoftGumbelQuantizedDOELayerv3(doe_params, optim_params, device="cpu")
+    asm3 = ref.ASM.ASM_prop(z_distance=200 * MM, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True,
+                            device="cpu")
+    w0 = doe.weight_init_phase.detach().numpy().copy()
+    opt = torch.optim.Adam(doe.parameters(), lr=0.02)
+    mse = torch.nn.MSELoss()
+    arrays = {"source": f0.data.detach().numpy(), "before_lens": f1.data.detach().numpy(),
+              "field_in": field_in.data.detach().numpy(), "target": target.numpy(), "w0": w0}
+    losses, kinds = [], []
+    torch.manual_seed(77)
+    for itr in range(steps):
+        with record_rng() as draws:
+            out, _ = quiet(lambda: asm3(doe(field_in, itr / steps)))
+        amp = HF.normalize(torch.abs(out.data) ** 2)
+        loss = mse(amp, target)
+        opt.zero_grad()
+        loss.backward()
+        if itr == 0:
+            arrays["grad0"] = doe.weight_init_phase.grad.numpy().copy()
+            arrays["out0"] = out.data.detach().numpy()
+        opt.step()
+        losses.append(float(loss.item()))
+        kinds.append([k for k, _ in draws])
+        for i, (k, v) in enumerate(draws):
+            arrays[f"step{itr}__draw{i}"] = v
+    arrays["w_final"] = doe.weight_init_phase.detach().numpy().copy()
+    arrays["losses"] = np.array(losses, dtype=np.float64)
+    manifest["qat"] = dict(steps=steps, doe_params=doe_params, optim_params=optim_params, f=300, lr=0.02,
+                           init_seed=2024, draws=kinds, foci_mm=FOCI, losses=losses)
+    np.savez_compressed(os.path.join(HERE, "qat_golden.npz"), **arrays)
+    print("qat losses", losses[:3], losses[-3:])
+
+
 def main():
     path = os.path.join(HERE, "manifest.json")
     if "--only" in sys.argv:
         which = sys.argv[sys.argv.index("--only") + 1]
         with open(path) as fh:
             manifest = json.load(fh)
-        {"doe_layers": gen_doe_layers}[which](manifest)
+        {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat}[which](manifest)
     else:
         manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
                     "asm": [], "czt": [], "rsc": [], "doe": []}
@@ -417,6 +541,8 @@ def main():
         gen_czt_rsc(manifest)
         gen_doe(manifest)
         gen_doe_layers(manifest)
+        gen_optics(manifest)
+        gen_qat(manifest)
     with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1, default=float)
 

@@ -1,0 +1,67 @@
+"""Multi-process paths on CPU (gloo, world_size 2): the QAT gradient all-reduce and the
+independent-plane sharding used by bench.py."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _allreduce_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quantizationawarethzdoe_amd.qat import GradientAllReduce
+        torch.manual_seed(0)
+        params = [torch.nn.Parameter(torch.zeros(50, 50)), torch.nn.Parameter(torch.zeros(3, 7)),
+                  torch.nn.Parameter(torch.zeros(4), requires_grad=False)]
+        g = torch.Generator().manual_seed(100 + rank)  # each rank: its own noise sample
+        for p in params[:2]:
+            p.grad = torch.randn(p.shape, generator=g)
+        local = [p.grad.clone() for p in params[:2]]
+        ar = GradientAllReduce(params)
+        assert ar.world == world and len(ar.params) == 2
+        ar()
+        gathered = [[torch.zeros_like(t) for _ in range(world)] for t in local]
+        for t, out in zip(local, gathered):
+            dist.all_gather(out, t)
+        ok = all(torch.allclose(p.grad, torch.stack(out).mean(0), atol=1e-7)
+                 for p, out in zip(params[:2], gathered))
+        # a parameter without a gradient contributes zeros and receives the average
+        params[1].grad = None
+        ar()
+        q.put((rank, ok, params[1].grad is not None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_allreduce_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_allreduce_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok and has for _, ok, has in res), res
+
+
+def test_plane_sharding_covers_every_plane_once():
+    from bench import shard_planes
+    for n_planes in (1, 7, 64, 512):
+        for world in (1, 2, 3, 8):
+            seen = []
+            for r in range(world):
+                seen.extend(shard_planes(n_planes, r, world))
+            assert sorted(seen) == list(range(n_planes))

@@ -195,3 +195,70 @@ def test_doe_layer_oracle_matches_reference(case):
     (out.abs() ** 2).sum().backward()
     g = A[f"{k}__gw"]
     assert rel_l2(w.grad.numpy(), g) <= 1e-5 or np.abs(g).max() == np.abs(w.grad.numpy()).max() == 0
+
+
+OPT = M.get("optics", [])
+
+
+@pytest.mark.parametrize("case", OPT, ids=[c["name"] for c in OPT])
+def test_optics_oracle_matches_reference(case):
+    A = arrays("optics")
+    k = case["name"]
+    if case["kind"] == "gauss":
+        kw = case["kw"]
+        lam = wavelengths(case["f"])
+        H, W = kw["height"], kw["width"]
+        d = torch.tensor(case["dxy"], dtype=torch.float32)
+        o = orc.gaussian_beam(H, W, d, d, lam, kw.get("beam_waist_x"), kw.get("beam_waist_y"),
+                              center=kw.get("center", (0, 0)), z_w0=kw.get("z_w0", (0, 0)), alpha=kw.get("alpha", 0))
+        assert rel_l2(o.numpy(), A[f"{k}__out32"]) <= 1e-6
+        return
+    x = torch.from_numpy(A["field_in"]).requires_grad_(True)
+    lam = wavelengths(case["f"])
+    dx, dy = torch.tensor(case["dx"], dtype=torch.float32), torch.tensor(case["dy"], dtype=torch.float32)
+    if case["kind"] == "lens":
+        o = orc.thin_lens(x, dx, dy, case["arg"], lam)
+    else:
+        o = x * orc.aperture_mask(x.shape[-2], x.shape[-1], dx, dy, case["kind"], case["arg"])[None, None]
+    gx, = torch.autograd.grad(o, x, grad_outputs=torch.from_numpy(A["field_gout"]))
+    assert rel_l2(o.detach().numpy(), A[f"{k}__out32"]) <= 1e-6
+    assert rel_l2(gx.numpy(), A[f"{k}__gx32"]) <= 1e-6
+
+
+def test_loss_oracle_matches_reference():
+    A = arrays("optics")
+    E = torch.from_numpy(A["loss_in"]).requires_grad_(True)
+    loss = orc.intensity_mse(E, torch.from_numpy(A["loss_target"]))
+    g, = torch.autograd.grad(loss, E)
+    assert abs(float(loss) - float(A["loss_value"])) <= 1e-6 * float(A["loss_value"])
+    assert rel_l2(g.numpy(), A["loss_grad"]) <= 1e-5
+
+
+def test_qat_system_oracle_matches_reference():
+    """cfg4 optics before the DOE and the first QAT step (loss + weight gradient) via the oracle."""
+    A = arrays("qat")
+    q = M["qat"]
+    lam = wavelengths([q["f"]])
+    d = torch.tensor(1e-3, dtype=torch.float32)
+    src = orc.gaussian_beam(100, 100, d, d, lam)
+    assert rel_l2(src.numpy(), A["source"]) <= 1e-6
+    sp = torch.tensor([1e-3, 1e-3], dtype=torch.float32)
+    f1 = orc.asm_forward(src, lam, sp, 0.127, padding_scale=2)
+    assert rel_l2(f1.numpy(), A["before_lens"]) <= 1e-5
+    f2 = orc.thin_lens(f1, d, d, 0.127, lam)
+    f3 = f2 * orc.aperture_mask(100, 100, d, d, "rect", 0.08)[None, None]
+    assert rel_l2(f3.numpy(), A["field_in"]) <= 1e-5
+    dp, op = q["doe_params"], q["optim_params"]
+    w = torch.from_numpy(A["w0"]).requires_grad_(True)
+    lut = torch.linspace(0, torch.tensor(dp["height_constraint_max"]), dp["doe_level"] + 1)[:-1]
+    h = orc.layer_height_map("SoftGumbelQuantizedDOELayerv3", w, lut, torch.tensor(dp["height_constraint_max"]),
+                             lam.min(), dp["material"][0], 0.0, op, dp["num_unit"], dp["doe_size"])
+    mat = torch.tensor(dp["material"])
+    fm = orc.doe_modulate(torch.from_numpy(A["field_in"]), h, lam, mat[0], mat[1], tolerance=dp["tolerance"],
+                          noise_u01=torch.from_numpy(A["step0__draw0"]))
+    out = orc.asm_forward(fm, lam, sp, 0.2, padding_scale=2)
+    assert rel_l2(out.detach().numpy(), A["out0"]) <= 1e-5
+    loss = orc.intensity_mse(out, torch.from_numpy(A["target"]))
+    assert abs(float(loss) - q["losses"][0]) <= 1e-5 * q["losses"][0]
+    loss.backward()
+    assert rel_l2(w.grad.numpy(), A["grad0"]) <= 1e-4
