@@ -168,6 +168,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
     return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
   };
   if constexpr (PN > 0) {
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
     auto ld = [&](int, int, int idx) {
       const int s = idx - a.in_c0;
       return (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
@@ -176,7 +177,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
       const int c = band_col(j, PN, a.J, a.ncols);
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
-    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
+    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
@@ -216,12 +217,13 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
     constexpr int RL = S::radix(S::NST - 1, false);  // radix of the forward's last stage
     constexpr int MBL = PN / RL / TT;                // its butterflies per thread
     float2 sp[MBL][RL];                              // spectrum, element i + r*PN/RL
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), ph.tw, tid, nt);
     auto ld0 = [&](int, int, int idx) {
       const int s = idx - a.in_r0;
       return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, ph.tw, tid, ld0, sv0);
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
     if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
       int tz = threadIdx.x;
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
         const int r = j - a.out_r0;
         if (r >= 0 && r < a.Hout) dst[(size_t)r * CB] = cscale(v, a.scale);
       };
-      fft_pow2_io<true, PN, TT, true, false, false>(lds, ph.tw, tz, ld1, sv1);
+      fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tz, ld1, sv1);
       return;
     }
     // The evanescent and band-limit masks are monotone in |m_x| (every fp32 operation of
@@ -240,7 +242,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
     // exactly |m_x| <= M_z.  One lane per z finds M_z by bisection with the exact
     // reference-order tests; the per-element work is then sqrt once per column and one
     // sincos per z.
-    int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN));
+    int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN) + tw_lds_count(PN));
     const float kl = TWO_PI_F / lam;
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
@@ -289,7 +291,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
         const int r = j - a.out_r0;
         if (r >= 0 && r < a.Hout) dst[(size_t)r * CB] = cscale(v, a.scale);
       };
-      fft_pow2_io<true, PN, TT, true, false, false>(lds, ph.tw, tz, ld1, sv1);
+      fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tz, ld1, sv1);
     }
   } else {
     for (int i = tid; i < Ph; i += nt) {
@@ -338,6 +340,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   const float2* src = U + (size_t)plane * a.ncb * CB * a.Hout;
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
   if constexpr (PN > 0) {
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
     auto ld = [&](int, int, int j) {
       const int c = band_col(j, PN, a.J, a.ncols);
       return c >= 0 ? src[blk(c, r, a.Hout)] : make_float2(0.f, 0.f);
@@ -346,7 +349,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
       const int w = j - a.out_c0;
       if (w >= 0 && w < a.Wout) dst[w] = v;
     };
-    fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
+    fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);

@@ -49,6 +49,7 @@ inline int fft_threads(int n) {
   if (t < 64) t = 64;
   return t;
 }
-inline size_t fft_lds_bytes(int n) { return (size_t)lds_floats2(n) * sizeof(float2); }
+// data rows + the two-level twiddle table of the power-of-two kernels
+inline size_t fft_lds_bytes(int n) { return (size_t)(lds_floats2(n) + tw_lds_count(n)) * sizeof(float2); }
 
 }  // namespace thz

@@ -291,13 +291,33 @@ __device__ __noinline__ void stage_generic(float2* lds, int n, int L, int R, con
 // ---------------------------------------------------------------------------------------------
 // Twiddles w^r, r = 1..R-1, of w = exp(-+2 pi i k / (L R)): powers of two straight from the
 // table (independent loads), the rest by at most three dependent complex products.
-template <int R, bool INV>
-__device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, int kt, float2* w) {
+//
+// Twiddle sources: the global table (const float2*: L1/L2 loads, vmcnt waits) or a two-level
+// copy in LDS (TwLds: w^t = A[t mod 64] * B[t / 64], 64 + N/64 entries, ds_reads that never
+// wait behind the kernel's outstanding global stores).
+struct TwLds {
+  const float2* t;  // t[a] = w^a (a < 64), t[64 + b] = w^(64 b)
+};
+__device__ __forceinline__ float2 twat(const float2* __restrict__ p, int i) { return p[i]; }
+__device__ __forceinline__ float2 twat(const TwLds& s, int i) { return cmul(s.t[i & 63], s.t[64 + (i >> 6)]); }
+
+// LDS slots of the two-level table of a length-n transform (placed after the data rows)
+__host__ __device__ constexpr int tw_lds_count(int n) { return n >= 1024 ? 64 + n / 64 : 0; }
+
+// Fill the two-level table from the global one; visible after the first stage's barrier.
+template <int N>
+__device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__ tw, int tid, int nt) {
+  for (int i = tid; i < tw_lds_count(N); i += nt) dst[i] = tw[i < 64 ? i : (i - 64) * 64];
+  return TwLds{dst};
+}
+
+template <int R, bool INV, class Tw>
+__device__ __forceinline__ void twiddle_powers(const Tw& tw, int kt, float2* w) {
   // w[r] for r = 1..R-1 ; kt = k * (N / (L R)) is the table index of w^1
-  w[1] = tw[kt];
-  if constexpr (R >= 4) w[2] = tw[2 * kt];
-  if constexpr (R >= 8) w[4] = tw[4 * kt];
-  if constexpr (R >= 16) w[8] = tw[8 * kt];
+  w[1] = twat(tw, kt);
+  if constexpr (R >= 4) w[2] = twat(tw, 2 * kt);
+  if constexpr (R >= 8) w[4] = twat(tw, 4 * kt);
+  if constexpr (R >= 16) w[8] = twat(tw, 8 * kt);
   if (INV) {
 #pragma unroll
     for (int p = 1; p < R; p <<= 1) w[p].y = -w[p].y;
@@ -320,8 +340,8 @@ __device__ __forceinline__ void twiddle_powers(const float2* __restrict__ tw, in
 // For power-of-two N >= 256 every LDS access is base + compile-time offset:
 //   padx(i + r NB) = padx(i) + r NB + (r NB >> 4)       (NB % 16 == 0)
 //   padx(j + r L)  = padx(j) + r L  + (r L >> 4)        (L | 16 or 16 | L, L R >= 16 or L == 1)
-template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, class Ld, class Sv>
-__device__ __forceinline__ void stage_x(float2* lds, const float2* __restrict__ tw, int tid, Ld& ld, Sv& sv) {
+template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, class Tw, class Ld, class Sv>
+__device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
   constexpr int NB = N / R;
   constexpr int MB = NB / T;  // butterflies per thread (exact)
   static_assert(MB * T == NB, "pow2 plan must tile exactly");
@@ -398,8 +418,8 @@ struct NoIO {
 // Stages S .. NST-1 of a power-of-two transform.  Stage 0 reads through ld unless
 // FIRST_LDS; the final stage writes through sv unless LAST_LDS.
 template <bool INV, int N, int T, bool SMALL_FIRST, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1,
-          class Ld, class Sv>
-__device__ __forceinline__ void fft_pow2_io(float2* lds, const float2* __restrict__ tw, int tid, Ld& ld, Sv& sv) {
+          class Tw, class Ld, class Sv>
+__device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
   using P = Pow2Sched<N>;
   if constexpr (S < P::NST) {
     constexpr int R = P::radix(S, SMALL_FIRST);
@@ -411,8 +431,8 @@ __device__ __forceinline__ void fft_pow2_io(float2* lds, const float2* __restric
 }
 
 // Whole transform with the data in LDS (natural order in and out).
-template <bool INV, int N, int T>
-__device__ __forceinline__ void fft_pow2(float2* lds, const float2* __restrict__ tw, int tid) {
+template <bool INV, int N, int T, class Tw>
+__device__ __forceinline__ void fft_pow2(float2* lds, const Tw& tw, int tid) {
   NoIO io;
   fft_pow2_io<INV, N, T, false, true, true>(lds, tw, tid, io, io);
 }
