@@ -37,7 +37,8 @@ struct AsmArgs {
   int in_r0, in_c0, Hin, Win;     // input window inside the padded plane
   int out_r0, out_c0, Hout, Wout; // output window
   int ncols, J;                   // kept spectral columns, m_y = c - J
-  int ncb;                        // column blocks of CB columns (blocked T / U layout)
+  int ncb;                        // column blocks of CB columns (blocked T layout)
+  int ncbu;                       // column blocks of CBU columns (blocked U layout)
   int nz, zoff;                   // z-planes in this chunk, offset into zv
   int bl, adjoint;
   float dx, dy, scale;
@@ -214,7 +215,10 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
   if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = Geo<PN>::T;
-    constexpr int RL = S::radix(S::NST - 1, false);  // radix of the forward's last stage
+    // forward = small radix first (its twiddle-free first stage is the cheap one, run once per
+    // column); inverse = radix-16 first (twiddle-free, run per z) reading exactly the elements the
+    // forward's last radix-16 stage left in this thread's registers
+    constexpr int RL = S::radix(S::NST - 1, true);   // radix of the forward's last stage
     constexpr int MBL = PN / RL / TT;                // its butterflies per thread
     float2 sp[MBL][RL];                              // spectrum, element i + r*PN/RL
     const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), ph.tw, tid, nt);
@@ -223,18 +227,18 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
+    fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tid, ld0, sv0);
     if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
       auto ld1 = [&](int m, int r, int idx) { return cmul(sp[m][r], tcol[idx]); };
-      float2* dst = U + (size_t)bc * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
+      float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if (r >= 0 && r < a.Hout) dst[(size_t)r * CB] = cscale(v, a.scale);
+        if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
       };
-      fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tz, ld1, sv1);
+      fft_pow2_io<true, PN, TT, false, false, false>(lds, twl, tz, ld1, sv1);
       return;
     }
     // The evanescent and band-limit masks are monotone in |m_x| (every fp32 operation of
@@ -261,16 +265,6 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       }
       mz[threadIdx.x] = lo;
     }
-    float sq[MBL][RL];
-    asm volatile("" : "+v"(tid));
-#pragma unroll
-    for (int m = 0; m < MBL; ++m)
-#pragma unroll
-      for (int r = 0; r < RL; ++r) {
-        const float Kx = kfreq(freq_index(tid + m * TT + r * (PN / RL), PN), PN, a.dx);
-        const float d = tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2));
-        sq[m][r] = sqrtf(fmaxf(d, 0.0f));
-      }
     __syncthreads();  // mz visible
     for (int zz = 0; zz < a.nz; ++zz) {
       const float z = a.zv[a.zoff + zz];
@@ -282,16 +276,19 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       auto ld1 = [&](int m, int r, int idx) {
         const int mx = freq_index(idx, PN);
         if (mx > M || -mx > M) return make_float2(0.f, 0.f);
+        // sqrt(k^2 - Kx^2 - Ky^2) recomputed per z (register pressure of the radix-16 head)
+        const float Kx = kfreq(mx, PN, a.dx);
+        const float sq = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
         float sn, cs;
-        sincos_rad(tf_mul(z, sq[m][r]), &sn, &cs);
+        sincos_rad(tf_mul(z, sq), &sn, &cs);
         return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
       };
-      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
+      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if (r >= 0 && r < a.Hout) dst[(size_t)r * CB] = cscale(v, a.scale);
+        if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
       };
-      fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tz, ld1, sv1);
+      fft_pow2_io<true, PN, TT, false, false, false>(lds, twl, tz, ld1, sv1);
     }
   } else {
     for (int i = tid; i < Ph; i += nt) {
@@ -321,8 +318,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       }
       __syncthreads();
       fft_lds<true>(lds, ph, tm, nt);
-      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hout + blk(c, 0, a.Hout);
-      for (int r = tm; r < a.Hout; r += nt) dst[(size_t)r * CB] = cscale(lds[padx(a.out_r0 + r)], a.scale);
+      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      for (int r = tm; r < a.Hout; r += nt) dst[(size_t)r * CBU] = cscale(lds[padx(a.out_r0 + r)], a.scale);
     }
   }
 }
@@ -337,13 +334,13 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   const int row = xcd_rows(blockIdx.x, gridDim.x);  // row in [0, nz*BC*Hout)
   const int plane = row / a.Hout, r = row - plane * a.Hout;  // plane = zz*BC + bc
   const int tid = threadIdx.x, nt = blockDim.x;
-  const float2* src = U + (size_t)plane * a.ncb * CB * a.Hout;
+  const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
   if constexpr (PN > 0) {
     const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
     auto ld = [&](int, int, int j) {
       const int c = band_col(j, PN, a.J, a.ncols);
-      return c >= 0 ? src[blk(c, r, a.Hout)] : make_float2(0.f, 0.f);
+      return c >= 0 ? src[blk_u(c, r, a.Hout)] : make_float2(0.f, 0.f);
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int w = j - a.out_c0;
@@ -353,7 +350,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);
-      lds[padx(j)] = c >= 0 ? src[blk(c, r, a.Hout)] : make_float2(0.f, 0.f);
+      lds[padx(j)] = c >= 0 ? src[blk_u(c, r, a.Hout)] : make_float2(0.f, 0.f);
     }
     __syncthreads();
     fft_lds<true>(lds, pw, tid, nt);
@@ -447,7 +444,7 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
 // Host side
 // ---------------------------------------------------------------------------------------------
 struct AsmGeom {
-  int BC, Ph, Pw, ncols, J, ncb, Hin, Win, Hout, Wout, zc;
+  int BC, Ph, Pw, ncols, J, ncb, ncbu, Hin, Win, Hout, Wout, zc;
 };
 
 static int validate(const thz_asm_desc* d) {
@@ -518,12 +515,13 @@ static void geometry(const thz_asm_desc* d, AsmGeom* g) {
     g->J = J;
   }
   g->ncb = (g->ncols + CB - 1) / CB;
+  g->ncbu = (g->ncols + CBU - 1) / CBU;
   int zc = d->z_chunk > 0 ? d->z_chunk : 0;
   if (zc == 0) {
     // default: up to 16 z-planes per column pass (the forward column FFT and the T read are
     // shared by the chunk), U capped at 2.5 GiB of the 288 GB HBM.  Measured on cfg2:
     // z_chunk 1/4/8/16 -> 2006/2620/2753/2859 planes/s.
-    const double per_z = (double)g->BC * g->ncb * CB * g->Hout * sizeof(float2);
+    const double per_z = (double)g->BC * g->ncbu * CBU * g->Hout * sizeof(float2);
     zc = (int)std::max(1.0, std::min(16.0, std::floor((2560.0 * 1024 * 1024) / per_z)));
   }
   g->zc = std::min(zc, d->adjoint ? 1 : d->Z);
@@ -585,7 +583,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static size_t ws_bytes(const AsmGeom& g) {
   return align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)) +
-         align256((size_t)g.zc * g.BC * g.ncb * CB * g.Hout * sizeof(float2));
+         align256((size_t)g.zc * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2));
 }
 
 // K1 once, then (K2, K3) per z-chunk, on a prepared argument block.
@@ -676,6 +674,7 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
   }
   a.ncols = g.ncols;
   a.ncb = g.ncb;
+  a.ncbu = g.ncbu;
   a.J = g.J;
   a.bl = d->bandlimit;
   a.adjoint = d->adjoint;
@@ -731,6 +730,7 @@ static int rsc_plan(const thz_rsc_desc* d, RscPlan* p) {
   g.ncols = g.Pw;
   g.J = g.Pw / 2;
   g.ncb = (g.ncols + CB - 1) / CB;
+  g.ncbu = (g.ncols + CBU - 1) / CBU;
   g.zc = 1;
   RscKArgs& k = p->k;
   k.C = d->C;
@@ -743,7 +743,7 @@ static int rsc_plan(const thz_rsc_desc* d, RscPlan* p) {
   p->tk = align256((size_t)d->C * k.ncbK * CB * g.Ph * sizeof(float2));
   p->kf = align256((size_t)d->C * g.Pw * g.Ph * sizeof(float2));
   p->t = align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2));
-  p->u = align256((size_t)g.BC * g.ncb * CB * g.Hout * sizeof(float2));
+  p->u = align256((size_t)g.BC * g.ncbu * CBU * g.Hout * sizeof(float2));
   return THZ_OK;
 }
 
@@ -796,6 +796,7 @@ extern "C" int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out,
   a.out_r0 = d->H; a.out_c0 = d->W; a.Hout = g.Hout; a.Wout = g.Wout;
   a.ncols = g.ncols;
   a.ncb = g.ncb;
+  a.ncbu = g.ncbu;
   a.J = g.J;
   a.bl = THZ_BANDLIMIT_NONE;
   a.dx = d->dx;
