@@ -26,7 +26,11 @@ import torch
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-from _refimport import import_reference  # noqa: E402
+from _refimport import REF, import_reference  # noqa: E402
+
+
+def ref_path():
+    return REF
 
 C0 = 2.998e8
 MM = 1e-3
@@ -526,13 +530,66 @@ def gen_qat(manifest, steps=20):
     print("qat losses", losses[:3], losses[-3:])
 
 
+def gen_donn(manifest):
+    """cfg5: the 3-layer DONN of experiment_DONN_3_layers.ipynb (cells 1-3), notebook forward
+    semantics, on 4 local t10k digits; RNG draws recorded in order."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from quantizationawarethzdoe_amd.donn import read_idx_images, to_field_batch
+    AP = ref.import_module("Components.Aperture")
+    imgs = read_idx_images(os.path.join(ref_path(), "data/MNIST/raw/t10k-images-idx3-ubyte.gz"), 4)
+    u = to_field_batch(imgs)
+    wl = C0 / 300e9
+    doe_params = dict(doe_size=[100, 100], doe_dxy=1 * MM, doe_level=4, look_up_table=None, num_unit=None,
+                      height_constraint_max=1 * MM, tolerance=30e-6, material=[2.66, 0.003])
+    optim_params = dict(c_s=100, tau_max=2.5, tau_min=1.5)
+    arrays = {"u": u.numpy()}
+    manifest["donn"] = []
+    for name, q, iter_frac in [("donn_fp", None, None), ("donn_sgs", "sgs", 0.9)]:
+        torch.manual_seed(11)
+        if q is None:
+            does = [ref.DOE.FullPrecisionDOELayer(doe_params, device="cpu") for _ in range(3)]
+        else:
+            does = [ref.DOE.SoftGumbelQuantizedDOELayerv3(doe_params, optim_params, device="cpu") for _ in range(3)]
+        asm50 = ref.ASM.ASM_prop(z_distance=50 * MM, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True,
+                                 device="cpu")
+        asm20 = ref.ASM.ASM_prop(z_distance=20 * MM, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True,
+                                 device="cpu")
+        ap = AP.ApertureElement(aperture_type='rect', aperture_size=0.08)
+        for i, d in enumerate(does):
+            arrays[f"{name}__w{i}"] = next(iter(d.parameters())).detach().numpy().copy()
+        torch.manual_seed(12)
+        with record_rng() as draws:
+            amp = torch.ones(1, 1, 100, 100) * u
+            field0 = ref.ElectricField(data=amp * torch.exp(1j * torch.zeros_like(amp)), wavelengths=wl,
+                                       spacing=1 * MM, device="cpu")
+            inputs = ap(quiet(asm50, field0)[0])
+            for i in range(2):
+                f = does[i](inputs, iter_frac)
+                f = ap(quiet(asm20, f)[0])
+            f = does[2](inputs, iter_frac)
+            out, _ = quiet(asm50, f)
+        loss = (out.data.abs() ** 2).sum()
+        loss.backward()
+        arrays[f"{name}__out32"] = out.data.detach().numpy()
+        for i, d in enumerate(does):
+            g = next(iter(d.parameters())).grad
+            arrays[f"{name}__g{i}"] = (g if g is not None else torch.zeros(1)).numpy().copy()
+        for i, (k, v) in enumerate(draws):
+            arrays[f"{name}__draw{i}"] = v
+        manifest["donn"].append(dict(name=name, q_method=q, iter_frac=iter_frac, doe_params=doe_params,
+                                     optim_params=optim_params, f=300, draws=[k for k, _ in draws],
+                                     loss="sum |E|^2"))
+        print("donn", name, [k for k, _ in draws])
+    np.savez_compressed(os.path.join(HERE, "donn_golden.npz"), **arrays)
+
+
 def main():
     path = os.path.join(HERE, "manifest.json")
     if "--only" in sys.argv:
         which = sys.argv[sys.argv.index("--only") + 1]
         with open(path) as fh:
             manifest = json.load(fh)
-        {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat}[which](manifest)
+        {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat, "donn": gen_donn}[which](manifest)
     else:
         manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
                     "asm": [], "czt": [], "rsc": [], "doe": []}
@@ -543,6 +600,7 @@ def main():
         gen_doe_layers(manifest)
         gen_optics(manifest)
         gen_qat(manifest)
+        gen_donn(manifest)
     with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1, default=float)
 

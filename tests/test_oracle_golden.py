@@ -262,3 +262,42 @@ def test_qat_system_oracle_matches_reference():
     assert abs(float(loss) - q["losses"][0]) <= 1e-5 * q["losses"][0]
     loss.backward()
     assert rel_l2(w.grad.numpy(), A["grad0"]) <= 1e-4
+
+
+DONN = M.get("donn", [])
+
+
+@pytest.mark.parametrize("case", DONN, ids=[c["name"] for c in DONN])
+def test_donn_oracle_matches_reference(case):
+    """cfg5 notebook forward (every layer modulates the encoded input) composed from oracle pieces."""
+    A = arrays("donn")
+    k = case["name"]
+    dp = case["doe_params"]
+    lam = wavelengths([case["f"]])
+    sp = torch.tensor([1e-3, 1e-3], dtype=torch.float32)
+    d = torch.tensor(1e-3, dtype=torch.float32)
+    mask = orc.aperture_mask(100, 100, d, d, "rect", 0.08)[None, None]
+    u = torch.from_numpy(A["u"]).to(torch.complex64)
+    inputs = orc.asm_forward(u, lam, sp, 0.05, padding_scale=2) * mask
+    draws = iter([A[f"{k}__draw{i}"] for i in range(len(case["draws"]))])
+    kinds = iter(case["draws"])
+    lut = torch.linspace(0, torch.tensor(dp["height_constraint_max"]), dp["doe_level"] + 1)[:-1]
+    cls = "FullPrecisionDOELayer" if case["q_method"] is None else "SoftGumbelQuantizedDOELayerv3"
+    mat = torch.tensor(dp["material"])
+
+    def layer(i, field):
+        w = torch.from_numpy(A[f"{k}__w{i}"])
+        expo = None
+        if cls != "FullPrecisionDOELayer":
+            assert next(kinds) == "expo"
+            expo = torch.from_numpy(next(draws))
+        h = orc.layer_height_map(cls, w, lut, torch.tensor(dp["height_constraint_max"]), lam.min(), dp["material"][0],
+                                 case["iter_frac"], case["optim_params"], dp["num_unit"], dp["doe_size"], expo=expo)
+        assert next(kinds) == "unif"
+        return orc.doe_modulate(field, h.reshape(100, 100), lam, mat[0], mat[1], tolerance=dp["tolerance"],
+                                noise_u01=torch.from_numpy(next(draws)))
+
+    for i in range(2):
+        orc.asm_forward(layer(i, inputs), lam, sp, 0.02, padding_scale=2)  # computed and discarded (nb :194)
+    out = orc.asm_forward(layer(2, inputs), lam, sp, 0.05, padding_scale=2)
+    assert rel_l2(out.numpy(), A[f"{k}__out32"]) <= 1e-5
