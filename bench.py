@@ -83,6 +83,68 @@ def cpu_baseline(budget_s=12.0, max_planes=8):
                       f"oracle.thz_oracle.asm_forward, torch-CPU fp32, {threads} threads, {dt:.1f} s"}
 
 
+def bench_czt(dev, rank, world, steps=10, warmup=2, dist=None):
+    """cfg3 (secondary line): CZT 2048^2 -> 512^2 zoom (dx 0.5 -> 0.25 mm, z 0.5 m) of a Gaussian
+    beam (w 20 mm) at 32 wavelengths c0 / linspace(220, 330 GHz); the wavelengths are sharded
+    over the ranks (strong scaling, no collective)."""
+    from quantizationawarethzdoe_amd.propagation import czt_apply
+    from quantizationawarethzdoe_amd.optics import gaussian_beam
+    freqs = torch.linspace(220e9, 330e9, 32, dtype=torch.float64)
+    lam_all = [float(torch.tensor(C0 / float(f), dtype=torch.float32)) for f in freqs]
+    mine = [lam_all[i] for i in shard_planes(32, rank, world)]
+    if not mine:
+        return None
+    x = gaussian_beam(2048, 2048, 0.5e-3, 0.5e-3, mine, [20e-3] * len(mine), [20e-3] * len(mine), device=dev)
+    sp = [float(torch.tensor(0.5e-3, dtype=torch.float32))] * 2
+    for _ in range(warmup):
+        czt_apply(x, mine, sp, 0.5, 512, 512, 0.25e-3, 0.25e-3)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        czt_apply(x, mine, sp, 0.5, 512, 512, 0.25e-3, 0.25e-3)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return {"workload": "cfg3: CZT_prop 2048^2 -> 512^2, 32 wavelengths 220-330 GHz sharded over ranks",
+            "value": round(32 * steps / dt, 2), "unit": "propagations/s", "ms_per_call": round(dt / steps * 1e3, 3),
+            "scaling": "strong"}
+
+
+def bench_qat(dev, rank, world, steps=60, dist=None):
+    """cfg4 (secondary line): four-focal-spots QAT iterations/s in each schedule phase (iter_frac
+    <= 0.3 continuous, 0.3-0.8 blend, > 0.8 quantized), with the one-bucket gradient all-reduce
+    across ranks (each rank its own noise sample)."""
+    from quantizationawarethzdoe_amd import qat
+    torch.manual_seed(1234 + rank)
+    system = qat.FourFocalSpotsSystem(device=dev)
+    trainer = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=6000)
+    out = {}
+    for name, frac in (("continuous", 0.1), ("blend", 0.5), ("quantized", 0.9)):
+        for _ in range(5):
+            trainer.step(frac)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = trainer.step(frac)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out[name] = {"it_per_s": round(steps / dt, 1), "ms_per_it": round(dt / steps * 1e3, 3),
+                     "loss": round(float(loss.detach()), 6)}
+    return {"workload": "cfg4: four_focal_spots QAT step (v3 DOE 100^2, ASM P=300, fused loss, Adam), "
+                        "gradient all-reduce over ranks", "phases": out}
+
+
 def load_traffic():
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -102,6 +164,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--z-chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 secondary measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -190,6 +253,9 @@ def main():
                     for k, v in stats.items()},
         "roofline": roof,
     }
+    if not args.headline_only:
+        line["secondary"] = {"cfg3_czt": bench_czt(dev, rank, world, dist=dist),
+                             "cfg4_qat": bench_qat(dev, rank, world, dist=dist)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -5,7 +5,7 @@ set -u
 out=${1:-gpurun_out/prof}; shift || true
 export TMPDIR=/tmp
 mkdir -p "$out"
-B="bench.py --steps 2 --warmup 1 --no-cpu-baseline $*"
+B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --headline-only $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 $B > "$out/trace.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- python3 $B > "$out/fetch.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- python3 $B > "$out/write.log" 2>&1 || exit $?
