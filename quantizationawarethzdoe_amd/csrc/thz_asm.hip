@@ -338,13 +338,23 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
   if constexpr (PN > 0) {
     const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
-    auto ld = [&](int, int, int j) {
-      const int c = band_col(j, PN, a.J, a.ncols);
-      return c >= 0 ? src[blk_u(c, r, a.Hout)] : make_float2(0.f, 0.f);
+    // First stage (radix 16, L = 1) reads j = i + q*NB0, i < NB0.  Its band column is
+    // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
+    // frequencies), a multiple of CBU: the blocked address is then base(c0) + delta_q*Hout,
+    // one add per element instead of the full blk_u() per element.
+    constexpr int NB0 = PN / 16;
+    static_assert(NB0 % CBU == 0, "band offsets must be whole U blocks");
+    static_assert(Geo<PN>::T == NB0, "one first-stage butterfly per thread: i = tid");
+    const int c0 = tid + a.J;
+    const float2* base = src + ((long)(c0 / CBU) * a.Hout + r) * CBU + (c0 % CBU);
+    auto ld = [&](int, int q, int) {
+      const int delta = q * NB0 >= PN / 2 ? q * NB0 - PN : q * NB0;
+      if ((unsigned)(c0 + delta) >= (unsigned)a.ncols) return make_float2(0.f, 0.f);
+      return base[(long)delta * a.Hout];
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int w = j - a.out_c0;
-      if (w >= 0 && w < a.Wout) dst[w] = v;
+      if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
     };
     fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
   } else {
@@ -385,9 +395,10 @@ __global__ void __launch_bounds__(1024) rsc_k_rows(float2* __restrict__ TK, FftP
   auto store = [&](int j, float2 v) { dst[blk(band_col(j, k.Pw, k.Pw / 2, k.Pw), i, k.Ph)] = v; };
   const int tid = threadIdx.x, nt = blockDim.x;
   if constexpr (PN > 0) {
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
     auto ld = [&](int, int, int j) { return load(j); };
     auto sv = [&](int, int, int j, float2 v) { store(j, v); };
-    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, pw.tw, tid, ld, sv);
+    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < k.Pw; j += nt) lds[padx(j)] = load(j);
     __syncthreads();
@@ -406,9 +417,10 @@ __global__ void __launch_bounds__(1024) rsc_k_cols(const float2* __restrict__ TK
   float2* dst = KF + ((size_t)c * k.Pw + cc) * k.Ph;
   const int tid = threadIdx.x, nt = blockDim.x;
   if constexpr (PN > 0) {
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), ph.tw, tid, nt);
     auto ld = [&](int, int, int i) { return col[(size_t)i * CB]; };
     auto sv = [&](int, int, int i, float2 v) { dst[i] = v; };
-    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, ph.tw, tid, ld, sv);
+    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
   } else {
     for (int i = tid; i < k.Ph; i += nt) lds[padx(i)] = col[(size_t)i * CB];
     __syncthreads();
@@ -427,10 +439,11 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
   const int tid = threadIdx.x, nt = blockDim.x;
   const size_t base = (size_t)blockIdx.x * p.n;
   if constexpr (PN > 0) {
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), p.tw, tid, nt);
     auto ld = [&](int, int, int j) { return in[base + j]; };
     auto sv = [&](int, int, int j, float2 v) { out[base + j] = v; };
-    if (inverse) fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, p.tw, tid, ld, sv);
-    else fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, p.tw, tid, ld, sv);
+    if (inverse) fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
+    else fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];
     __syncthreads();

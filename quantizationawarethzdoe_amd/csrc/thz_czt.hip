@@ -139,13 +139,14 @@ __global__ void __launch_bounds__(1024) czt_rows(const float2* __restrict__ in, 
     constexpr int RL = S::radix(S::NST - 1, false);
     constexpr int MBL = PN / RL / TT;
     float2 sp[MBL][RL];
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pl.tw, tid, blockDim.x);
     auto ld0 = [&](int, int, int idx) { return load_x(idx); };
     auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, pl.tw, tid, ld0, sv0);
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
     asm volatile("" : "+v"(tid));
     auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
     auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    fft_pow2_io<true, PN, TT, true, false, false>(lds, pl.tw, tid, ld1, sv1);
+    fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tid, ld1, sv1);
   } else {
     const int n = pl.n, nt = blockDim.x;
     for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
@@ -196,13 +197,14 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
     constexpr int RL = S::radix(S::NST - 1, false);
     constexpr int MBL = PN / RL / TT;
     float2 sp[MBL][RL];
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pl.tw, tid, blockDim.x);
     auto ld0 = [&](int, int, int idx) { return load_x(idx); };
     auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, pl.tw, tid, ld0, sv0);
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
     asm volatile("" : "+v"(tid));
     auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
     auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    fft_pow2_io<true, PN, TT, true, false, false>(lds, pl.tw, tid, ld1, sv1);
+    fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tid, ld1, sv1);
   } else {
     const int n = pl.n, nt = blockDim.x;
     for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);

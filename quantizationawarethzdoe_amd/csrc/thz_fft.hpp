@@ -304,10 +304,17 @@ __device__ __forceinline__ float2 twat(const TwLds& s, int i) { return cmul(s.t[
 // LDS slots of the two-level table of a length-n transform (placed after the data rows)
 __host__ __device__ constexpr int tw_lds_count(int n) { return n >= 1024 ? 64 + n / 64 : 0; }
 
-// Fill the two-level table from the global one; visible after the first stage's barrier.
+// Fill the two-level table (visible after the first stage's barrier).  Generated in place with
+// double-precision sincospi -- the same values as the host table, without a global load whose
+// latency every workgroup would pay before issuing its data loads.
 template <int N>
-__device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__ tw, int tid, int nt) {
-  for (int i = tid; i < tw_lds_count(N); i += nt) dst[i] = tw[i < 64 ? i : (i - 64) * 64];
+__device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__, int tid, int nt) {
+  for (int i = tid; i < tw_lds_count(N); i += nt) {
+    const int t = i < 64 ? i : (i - 64) * 64;
+    double sn, cs;
+    sincospi(-2.0 * (double)t / (double)N, &sn, &cs);
+    dst[i] = make_float2((float)cs, (float)sn);
+  }
   return TwLds{dst};
 }
 
