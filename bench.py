@@ -122,7 +122,7 @@ def bench_qat(dev, rank, world, steps=60, dist=None):
     from quantizationawarethzdoe_amd import qat
     torch.manual_seed(1234 + rank)
     system = qat.FourFocalSpotsSystem(device=dev)
-    trainer = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=6000)
+    trainer = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=6000, graph=True)
     out = {}
     for name, frac in (("continuous", 0.1), ("blend", 0.5), ("quantized", 0.9)):
         for _ in range(5):
@@ -142,7 +142,7 @@ def bench_qat(dev, rank, world, steps=60, dist=None):
         out[name] = {"it_per_s": round(steps / dt, 1), "ms_per_it": round(dt / steps * 1e3, 3),
                      "loss": round(float(loss.detach()), 6)}
     return {"workload": "cfg4: four_focal_spots QAT step (v3 DOE 100^2, ASM P=300, fused loss, Adam), "
-                        "gradient all-reduce over ranks", "phases": out}
+                        "HIP-graph replay per schedule phase, gradient all-reduce over ranks", "phases": out}
 
 
 def load_traffic():

@@ -177,6 +177,8 @@ typedef struct thz_quant_desc {
   float s;            /* SGV3 steepness tau_max / tau */
   float beta;         /* SGV3 blend (iter_frac - 0.3) / 0.5 */
   float phase_scale;  /* SGV3 2 pi / lambda_min * (sqrt(eps) - 1), fp32 */
+  const float* dyn;   /* optional DEVICE [3] = (tau, s, beta) read by the kernels instead of the
+                         fields above, so one captured HIP graph serves every schedule step */
 } thz_quant_desc;
 
 int thz_quant_forward(const thz_quant_desc* d, const float* weight, const float* noise_exp, float* height_full,

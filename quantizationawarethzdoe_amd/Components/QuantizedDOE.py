@@ -87,6 +87,12 @@ class DOELayer(nn.Module):
     def build_height_map(self):
         return NotImplemented
 
+    def _dyn_values(self, iter_frac):  # layers without a temperature schedule
+        return 1.0, 0.0, 0.0
+
+    def _graph_phase(self, iter_frac):
+        return 0
+
     def modulate(self, input_field, preprocessed_height_map, height_tolerance, epsilon, tand) -> ElectricField:
         """Noise + nearest upsampling + transmission + product in one kernel (:92-126)."""
         h = preprocessed_height_map
@@ -141,8 +147,9 @@ class DOELayer(nn.Module):
         return lut
 
     def _quantize(self, kind, weight, mirror, clamp, expo=None, **kw):
+        # _dyn: device (tau, s, beta) installed by a graph-capturing trainer (qat.QATTrainer)
         return _doe.quantize(kind, weight, self._lut_values(), self._hmax, clamp=clamp, mirror=mirror, expo=expo,
-                             **kw)
+                             dyn=self.__dict__.get("_dyn"), **kw)
 
     def _gumbel_noise(self, shape, like):
         """The Exp(1) draw F.gumbel_softmax makes (torch.empty_like(logits).exponential_())."""
@@ -297,9 +304,25 @@ class _ScoreGumbelBase(DOELayer):
         hm = self.preprocessed_height_map(wavelengths=field.wavelengths, tau=tau, iter_frac=iter_frac)
         return self.modulate(field, hm, self.tolerance, self.epsilon, self.tand)
 
+    # -- graph replay support (qat.QATTrainer(graph=True)) -------------------------------------
+    def _dyn_values(self, iter_frac):
+        """(tau, s, beta) the quantizer kernels read from device memory at this schedule point."""
+        tau = _cos_tau(iter_frac, self.tau_min, self.tau_max)
+        beta = 0.0
+        if 0.3 < iter_frac <= 0.8:
+            beta = iter_frac if getattr(self, "_blend_by_iter_frac", False) else (iter_frac - 0.3) / (0.8 - 0.3)
+        return tau, self.tau_max / tau, beta
+
+    def _graph_phase(self, iter_frac):
+        """Schedule phases with different op sequences (each gets its own captured graph)."""
+        return 0 if iter_frac <= 0.3 else (1 if iter_frac <= 0.8 else 2)
+
 
 class SoftGumbelQuantizedDOELayer(_ScoreGumbelBase):
     """v1: the weight is a phase in [-pi, pi); scores against the LUT phases, Gumbel pick (:303-475)."""
+
+    def _graph_phase(self, iter_frac):
+        return 0
 
     def build_init_phase(self):
         height, width = self.doe_size[0], self.doe_size[1]
@@ -325,6 +348,9 @@ class SoftGumbelQuantizedDOELayer(_ScoreGumbelBase):
 
 class SoftGumbelQuantizedDOELayerv2(_ScoreGumbelBase):
     """v2: sigmoid height, quantized by score-Gumbel once iter_frac > 0.5 (:478-656)."""
+
+    def _graph_phase(self, iter_frac):
+        return int(iter_frac > 0.5)
 
     def build_init_phase(self):
         height, width = self.doe_size[0], self.doe_size[1]
@@ -407,6 +433,12 @@ class NaiveGumbelQuantizedDOELayer(_ScoreGumbelBase):
         tau = _cos_tau(iter_frac, self.tau_min, self.tau_max) if iter_frac is not None else None
         return self.modulate(field, self.preprocessed_height_map(tau=tau), self.tolerance, self.epsilon, self.tand)
 
+    def _dyn_values(self, iter_frac):
+        return _cos_tau(iter_frac, self.tau_min, self.tau_max), 0.0, 0.0
+
+    def _graph_phase(self, iter_frac):
+        return 0
+
 
 class PSQuantizedDOELayer(DOELayer):
     """Progressive sigmoid quantization: sum of L-1 tempered sigmoids (:1068-1236)."""
@@ -441,6 +473,12 @@ class PSQuantizedDOELayer(DOELayer):
     def forward(self, field: ElectricField, iter_frac=None) -> ElectricField:
         tau = _linear_tau(iter_frac, self.tau_min, self.tau_max) if iter_frac is not None else None
         return self.modulate(field, self.preprocessed_height_map(tau=tau), self.tolerance, self.epsilon, self.tand)
+
+    def _dyn_values(self, iter_frac):
+        return _linear_tau(iter_frac, self.tau_min, self.tau_max), 0.0, 0.0
+
+    def _graph_phase(self, iter_frac):
+        return 0
 
 
 class STEQuantizationFunction(torch.autograd.Function):

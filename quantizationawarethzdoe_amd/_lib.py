@@ -89,7 +89,7 @@ class QuantDesc(ctypes.Structure):
         ("L", ctypes.c_int), ("lut", ctypes.POINTER(ctypes.c_float)),
         ("hmax", ctypes.c_float), ("clamp", ctypes.c_float), ("tau", ctypes.c_float),
         ("iter_frac", ctypes.c_float), ("c_s", ctypes.c_float), ("s", ctypes.c_float),
-        ("beta", ctypes.c_float), ("phase_scale", ctypes.c_float),
+        ("beta", ctypes.c_float), ("phase_scale", ctypes.c_float), ("dyn", ctypes.c_void_p),
     ]
 
 

@@ -127,6 +127,7 @@ __global__ void doe_modulate_bwd(const float2* __restrict__ g, const float2* __r
 struct QArgs {
   int kind, hq, wq, mirror, L;
   float hmax, clampv, tau, iter_frac, c_s, s, beta, phase_scale;
+  const float* dyn;  // device (tau, s, beta) overriding the three above (graph replay)
   float lut[THZ_MAX_LUT];
   float plut_w[THZ_MAX_LUT];  // wrapped phase LUT (SGV3)
 };
@@ -206,8 +207,17 @@ __device__ __forceinline__ float st_value(const QArgs& a, const float* y, int ar
   return q;
 }
 
+__device__ __forceinline__ void apply_dyn(QArgs& a) {
+  if (a.dyn) {
+    a.tau = a.dyn[0];
+    a.s = a.dyn[1];
+    a.beta = a.dyn[2];
+  }
+}
+
 __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __restrict__ expo,
                           float* __restrict__ hfull, float* __restrict__ ysave) {
+  apply_dyn(a);
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = a.hq * a.wq;
   if (p >= n) return;
@@ -269,6 +279,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
 
 __global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __restrict__ ysave,
                           const float* __restrict__ gfull, float* __restrict__ gw) {
+  apply_dyn(a);
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = a.hq * a.wq;
   if (p >= n) return;
@@ -352,6 +363,7 @@ static int qargs(const thz_quant_desc* d, QArgs* a) {
   a->s = d->s;
   a->beta = d->beta;
   a->phase_scale = d->phase_scale;
+  a->dyn = d->dyn;
   for (int l = 0; l < d->L; ++l) {
     a->lut[l] = d->lut[l];
     // (phase_lut + pi) % 2pi - pi of the reference's LUT phases (:802), host fp32

@@ -78,12 +78,12 @@ def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None):
 
 
 def _quant_desc(kind, hq, wq, mirror, lut, hmax, clamp, tau=1.0, iter_frac=0.0, c_s=0.0, s=0.0, beta=0.0,
-                phase_scale=0.0):
+                phase_scale=0.0, dyn=None):
     arr = _lib.float_array(lut)
     d = _lib.QuantDesc(kind=kind, hq=hq, wq=wq, mirror=int(bool(mirror)), L=len(lut),
                        lut=ctypes.cast(arr, ctypes.POINTER(ctypes.c_float)), hmax=float(hmax), clamp=float(clamp),
                        tau=float(tau), iter_frac=float(iter_frac), c_s=float(c_s), s=float(s), beta=float(beta),
-                       phase_scale=float(phase_scale))
+                       phase_scale=float(phase_scale), dyn=dyn.data_ptr() if dyn is not None else None)
     d._keep = arr
     return d
 
@@ -116,8 +116,11 @@ class _Quantize(torch.autograd.Function):
         return gw, None, None
 
 
-def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, **kw):
-    """Quantized height map of one of the QAT layers (HIP forward + backward); weight shape kept."""
+def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, dyn=None, **kw):
+    """Quantized height map of one of the QAT layers (HIP forward + backward); weight shape kept.
+
+    ``dyn``: optional device float32 [3] = (tau, s, beta) the kernels read instead of the
+    keyword values, so a captured graph can be replayed across schedule steps."""
     _require_device(weight, "DOE quantizer")
     shape = weight.shape
     if kind == _lib.Q_NGS:
@@ -128,8 +131,10 @@ def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, **kw):
         hq, wq = shape[-2], shape[-1]
     if len(lut) > _lib.THZ_MAX_LUT:
         raise ValueError(f"at most {_lib.THZ_MAX_LUT} LUT levels")
+    if dyn is not None and (dyn.dtype != torch.float32 or not dyn.is_cuda or dyn.numel() != 3):
+        raise ValueError("dyn must be a float32 device tensor of 3 values (tau, s, beta)")
     cfg = (kind, int(hq), int(wq), bool(mirror), tuple(float(v) for v in lut),
-           dict(hmax=float(hmax), clamp=float(clamp), **{k: float(v) for k, v in kw.items()}))
+           dict(hmax=float(hmax), clamp=float(clamp), dyn=dyn, **{k: float(v) for k, v in kw.items()}))
     e = expo.contiguous().float() if expo is not None else None
     return _Quantize.apply(weight.reshape(shape), e, cfg)
 

@@ -143,25 +143,111 @@ class GradientAllReduce:
 
 
 class QATTrainer:
-    """One QAT iteration = forward, fused loss, backward, gradient all-reduce, Adam step."""
+    """One QAT iteration = forward, fused loss, backward, gradient all-reduce, Adam step.
 
-    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None):
+    ``graph=True`` captures the iteration as HIP graphs (one per schedule phase of the DOE
+    layer: continuous / blend / quantized for v3) and replays them: the step is launch-bound
+    at cfg4 sizes (100^2, P = 300; ~30 small kernels), so replay removes the per-kernel host
+    overhead.  The schedule values that change every step (tau, s = tau_max / tau, beta) reach
+    the quantizer kernels through a 3-float device buffer (thz_quant_desc.dyn), and the
+    Gumbel / height-noise draws are graph-safe philox draws, so each replay is a fresh sample.
+    With N ranks the replay is split around the (eager) gradient all-reduce.  The random
+    stream differs from the eager path (same distribution, different draws).
+    """
+
+    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False):
         self.system = system
         self.target = target.to(system.device).float().contiguous()
         self.max_itrs = max_itrs
-        self.optimizer = torch.optim.Adam(system.parameters(), lr=lr)
+        self.graph = graph
+        self.optimizer = torch.optim.Adam(system.parameters(), lr=lr, capturable=graph)
         self.allreduce = GradientAllReduce(list(system.parameters()), group=group)
         self.itr = 0
+        self._graphs = {}
+        if graph:
+            self.dyn = torch.zeros(3, dtype=torch.float32, device=system.device)
+            system.doe._dyn = self.dyn
+
+    def _frac(self, iter_frac):
+        return self.itr / self.max_itrs if iter_frac is None else iter_frac
 
     def step(self, iter_frac=None):
-        frac = self.itr / self.max_itrs if iter_frac is None else iter_frac
+        frac = self._frac(iter_frac)
+        if self.graph:
+            loss = self._graph_step(frac)
+        else:
+            out = self.system(frac)
+            loss = _optics.intensity_mse(out.data, self.target)
+            self.optimizer.zero_grad(set_to_none=False)
+            loss.backward()
+            self.allreduce()
+            self.optimizer.step()
+        self.itr += 1
+        return loss
+
+    # -- graph path ----------------------------------------------------------------------------
+    def _fwd_bwd(self, frac):
         out = self.system(frac)
         loss = _optics.intensity_mse(out.data, self.target)
-        self.optimizer.zero_grad(set_to_none=False)
         loss.backward()
-        self.allreduce()
-        self.optimizer.step()
-        self.itr += 1
+        return loss
+
+    def _capture(self, frac):
+        params = self.allreduce.params
+        # warm-up steps (allocator, autograd, Adam's lazy state) must not change the training
+        # trajectory: snapshot the weights and the optimiser state, restore them afterwards
+        p0 = [p.detach().clone() for p in params]
+        st0 = {id(p): {k: v.clone() for k, v in self.optimizer.state[p].items() if torch.is_tensor(v)}
+               for p in params if p in self.optimizer.state}
+        side = torch.cuda.Stream(device=self.system.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                self.optimizer.zero_grad(set_to_none=True)
+                self._fwd_bwd(frac)
+                self.optimizer.step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        with torch.no_grad():
+            for p, v in zip(params, p0):
+                p.copy_(v)
+            for p in params:
+                saved = st0.get(id(p))
+                for k, v in self.optimizer.state[p].items():
+                    if torch.is_tensor(v):
+                        v.copy_(saved[k]) if saved is not None else v.zero_()
+        self.optimizer.zero_grad(set_to_none=True)
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            loss = self._fwd_bwd(frac)
+            if self.allreduce.world > 1:
+                off = 0
+                for p in params:
+                    k = p.numel()
+                    self.allreduce.flat[off:off + k].copy_(p.grad.reshape(-1))
+                    off += k
+        with torch.cuda.graph(g_opt):
+            if self.allreduce.world > 1:
+                off = 0
+                for p in params:
+                    k = p.numel()
+                    p.grad.copy_(self.allreduce.flat[off:off + k].view_as(p))
+                    off += k
+            self.optimizer.step()
+        return g_fb, g_opt, loss
+
+    def _graph_step(self, frac):
+        phase = self.system.doe._graph_phase(frac)
+        tau, sv, beta = self.system.doe._dyn_values(frac)
+        self.dyn.copy_(torch.tensor([tau, sv, beta], dtype=torch.float32))
+        if phase not in self._graphs:
+            self._graphs[phase] = self._capture(frac)
+        g_fb, g_opt, loss = self._graphs[phase]
+        g_fb.replay()
+        if self.allreduce.world > 1:
+            dist.all_reduce(self.allreduce.flat, op=dist.ReduceOp.SUM, group=self.allreduce.group)
+            self.allreduce.flat.mul_(1.0 / self.allreduce.world)
+        g_opt.replay()
         return loss
 
     def train(self, steps, log_every=200, log=print):

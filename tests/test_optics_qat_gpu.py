@@ -204,3 +204,31 @@ def test_donn_chained_runs_and_differs():
     b = model(u, chained=True).data
     assert a.shape == b.shape == (2, 1, 100, 100)
     assert torch.isfinite(b.abs()).all() and not torch.allclose(a, b)
+
+
+def test_qat_graph_replay_matches_eager_with_fixed_noise():
+    """Graph-captured QAT steps (dyn schedule buffer) == eager steps when the noise is fixed:
+    the Gumbel / tolerance draws are replaced by constant tensors in both paths."""
+    from quantizationawarethzdoe_amd import qat
+    g = torch.Generator().manual_seed(9)
+    expo = torch.empty(1, 4, 50, 50).exponential_(generator=g).to(_dev())
+    unif = torch.rand(100, 100, generator=g).to(_dev())
+    w0 = torch.randn(50, 50, generator=g)
+    target = qat.four_focal_spots_target(device=_dev())
+    losses = {}
+    weights = {}
+    for graph in (False, True):
+        system = qat.FourFocalSpotsSystem(device=_dev())
+        with torch.no_grad():
+            system.doe.weight_init_phase.copy_(w0)
+        system.doe._gumbel_noise = lambda shape, like: expo.clone()
+        orig = torch.rand_like
+        torch.rand_like = lambda t, *a, **k: unif.clone()
+        try:
+            tr = qat.QATTrainer(system, target, max_itrs=20, graph=graph)
+            losses[graph] = [float(tr.step().detach()) for _ in range(20)]
+        finally:
+            torch.rand_like = orig
+        weights[graph] = system.doe.weight_init_phase.detach().cpu().numpy()
+    np.testing.assert_allclose(losses[True], losses[False], rtol=1e-4)
+    assert rel_l2(weights[True], weights[False]) <= 1e-4
