@@ -171,10 +171,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # test knobs for rehearsing N > 1 on a one-GPU box: every rank on cuda:0 over gloo
+    if os.environ.get("THZ_BENCH_SAME_DEVICE"):
+        local = 0
+    backend = os.environ.get("THZ_BENCH_BACKEND", "nccl")
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -254,8 +261,13 @@ def main():
         "roofline": roof,
     }
     if not args.headline_only:
-        line["secondary"] = {"cfg3_czt": bench_czt(dev, rank, world, dist=dist),
-                             "cfg4_qat": bench_qat(dev, rank, world, dist=dist)}
+        # secondary workloads never take the headline line down with them
+        line["secondary"] = {}
+        for key, fn in (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat)):
+            try:
+                line["secondary"][key] = fn(dev, rank, world, dist=dist)
+            except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+                line["secondary"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline()
     if rank == 0:
