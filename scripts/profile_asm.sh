@@ -6,7 +6,8 @@ out=${1:-gpurun_out/prof}; shift || true
 export TMPDIR=/tmp
 mkdir -p "$out"
 B="bench.py --steps 2 --warmup 1 --no-cpu-baseline --headline-only $*"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 $B > "$out/trace.log" 2>&1 || exit $?
+# the trace pass runs the bench's own default step counts so its averages match bench.py's
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --headline-only $* > "$out/trace.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$out/fetch" -o run --output-format csv -- python3 $B > "$out/fetch.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$out/write" -o run --output-format csv -- python3 $B > "$out/write.log" 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES SQ_WAVE_CYCLES -d "$out/sq" -o run --output-format csv -- python3 $B > "$out/sq.log" 2>&1 || exit $?
