@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
         const float Kx = kfreq(mx, PN, a.dx);
         const float sq = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
         float sn, cs;
-        sincos_rad(tf_mul(z, sq), &sn, &cs);
+        sincos_hw(tf_mul(z, sq), &sn, &cs);
         return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
       };
       float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);

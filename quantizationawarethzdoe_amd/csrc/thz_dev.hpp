@@ -119,6 +119,20 @@ __device__ __forceinline__ float2 rs_kernel(float x, float y, float z, float k, 
   return make_float2(cs * fr - sn * fi, cs * fi + sn * fr);
 }
 
+// sin/cos of an fp32 angle through the transcendental unit (v_sin_f32 / v_cos_f32 take
+// revolutions): ang / 2 pi split exactly into t + e with a two-constant product, reduced to
+// [-0.5, 0.5] revolutions.  Max abs error 1.8e-7 over |ang| <= 1000 rad against double
+// (sincos_rad: 6e-8; scripts/diag/hw_sincos_check.hip), at about half the instructions.
+__device__ __forceinline__ void sincos_hw(float ang, float* sn, float* cs) {
+  const float C_HI = 0.15915494f;          // fp32(1 / 2 pi)
+  const float C_LO = 6.4206383e-09f;       // 1 / 2 pi - C_HI
+  const float t = ang * C_HI;
+  const float e = __builtin_fmaf(ang, C_HI, -t) + ang * C_LO;
+  const float r = (t - __builtin_rintf(t)) + e;
+  *sn = __builtin_amdgcn_sinf(r);
+  *cs = __builtin_amdgcn_cosf(r);
+}
+
 // torch.linspace(start, end, n)[i] in fp32 (symmetric two-sided form of ATen's CPU kernel)
 __device__ __forceinline__ float lin(float start, float end, int n, int i) {
   if (n == 1) return start;

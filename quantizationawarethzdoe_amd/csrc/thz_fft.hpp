@@ -18,6 +18,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace thz {
 
 constexpr int FFT_MAX_STAGES = 24;
@@ -296,26 +298,32 @@ __device__ __noinline__ void stage_generic(float2* lds, int n, int L, int R, con
 // copy in LDS (TwLds: w^t = A[t mod 64] * B[t / 64], 64 + N/64 entries, ds_reads that never
 // wait behind the kernel's outstanding global stores).
 struct TwLds {
-  const float2* t;  // t[a] = w^a (a < 64), t[64 + b] = w^(64 b)
+  const float2* t;     // t[a] = w^a (a < 64), t[64 + b] = w^(64 b), w = exp(-2 pi i / N)
+  const float2* t256;  // exp(-2 pi i m / 256), m < 256: every twiddle of the L R = 256 stage
 };
 __device__ __forceinline__ float2 twat(const float2* __restrict__ p, int i) { return p[i]; }
 __device__ __forceinline__ float2 twat(const TwLds& s, int i) { return cmul(s.t[i & 63], s.t[64 + (i >> 6)]); }
 
-// LDS slots of the two-level table of a length-n transform (placed after the data rows)
-__host__ __device__ constexpr int tw_lds_count(int n) { return n >= 1024 ? 64 + n / 64 : 0; }
+// LDS slots of the twiddle tables of a length-n transform (placed after the data rows)
+__host__ __device__ constexpr int tw_lds_count(int n) { return n >= 1024 ? 64 + n / 64 + 256 : 0; }
 
-// Fill the two-level table (visible after the first stage's barrier).  Generated in place with
+// Fill the tables (visible after the first stage's barrier).  Generated in place with
 // double-precision sincospi -- the same values as the host table, without a global load whose
 // latency every workgroup would pay before issuing its data loads.
 template <int N>
 __device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__, int tid, int nt) {
+  constexpr int N2 = 64 + N / 64;
   for (int i = tid; i < tw_lds_count(N); i += nt) {
-    const int t = i < 64 ? i : (i - 64) * 64;
     double sn, cs;
-    sincospi(-2.0 * (double)t / (double)N, &sn, &cs);
+    if (i < N2) {
+      const int t = i < 64 ? i : (i - 64) * 64;
+      sincospi(-2.0 * (double)t / (double)N, &sn, &cs);
+    } else {
+      sincospi(-2.0 * (double)(i - N2) / 256.0, &sn, &cs);
+    }
     dst[i] = make_float2((float)cs, (float)sn);
   }
-  return TwLds{dst};
+  return TwLds{dst, dst + N2};
 }
 
 template <int R, bool INV, class Tw>
@@ -368,7 +376,17 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     }
     if constexpr (L > 1) {
       float2 w[R];
-      twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
+      if constexpr (L * R == 256 && std::is_same<Tw, TwLds>::value) {
+        // w^r = exp(-+2 pi i k r / 256) with k r <= 225: straight LDS reads, no products
+        const int k = i & (L - 1);
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          w[r] = tw.t256[k * r];
+          if (INV) w[r].y = -w[r].y;
+        }
+      } else {
+        twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
+      }
 #pragma unroll
       for (int r = 1; r < R; ++r) v[m][r] = cmul(v[m][r], w[r]);
     }
