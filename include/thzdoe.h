@@ -249,6 +249,19 @@ int thz_intensity_mse_backward(const thz_loss_desc* d, const void* field, const 
                                const float* grad_loss, void* grad_field, thz_stream_t stream);
 
 /*
+ * Field_Resampler.forward (Addons/Field_Resampler.py:74-118): bilinear grid_sample (zeros
+ * padding, align_corners=True) of [BC, Hin, Win] complex64 onto the centred output grid
+ * linspace(-((n-1)//2), (n-1)//2, n) * d_out, normalised by d_in * ((n_in - 1) // 2).
+ * The backward scatters grad_out with the same weights (grad_in is zeroed first).
+ */
+typedef struct thz_resample_desc {
+  int BC, Hin, Win, Hout, Wout;
+  float dx_in, dy_in, dx_out, dy_out;
+} thz_resample_desc;
+int thz_resample_forward(const thz_resample_desc* d, const void* in, void* out, thz_stream_t stream);
+int thz_resample_backward(const thz_resample_desc* d, const void* grad_out, void* grad_in, thz_stream_t stream);
+
+/*
  * Batched 1-D FFT along the contiguous axis (the building block of ft2/ift2,
  * utils/Helper_Functions.py:150, without shifts): in/out [rows, n], unnormalised,
  * inverse != 0 for the backward transform.  n <= 16384, any factorisation.

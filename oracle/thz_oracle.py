@@ -482,6 +482,26 @@ def intensity_mse(field, target):
     return torch.mean((amp - target.expand_as(amp)) ** 2)
 
 
+def resample(field, spacing, Hout, Wout, dx_out, dy_out):
+    """Field_Resampler.forward (Addons/Field_Resampler.py:56-118): bilinear grid_sample onto the
+    centred output grid (generateGrid, Helper_Functions.py:163-182), zeros, align_corners."""
+    B, C, H, W = field.shape
+    xc = torch.linspace(-((Hout - 1) // 2), (Hout - 1) // 2, Hout) * dx_out
+    yc = torch.linspace(-((Wout - 1) // 2), (Wout - 1) // 2, Wout) * dy_out
+    gX, gY = torch.meshgrid(xc, yc, indexing="ij")
+    dx = torch.tensor([spacing[0]])[:, None, None]
+    dy = torch.tensor([spacing[1]])[:, None, None]
+    xn = (dx * ((H - 1) // 2))[:, :, None, :]
+    yn = (dy * ((W - 1) // 2))[:, :, None, :]
+    grid = torch.stack([gY, gX], dim=-1).repeat(B, 1, 1, 1).to(field.real.dtype)
+    grid[..., 0] = grid[..., 0] / yn
+    grid[..., 1] = grid[..., 1] / xn
+    gs = torch.nn.functional.grid_sample
+    re = gs(field.real, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+    im = gs(field.imag, grid, mode="bilinear", padding_mode="zeros", align_corners=True)
+    return re + 1j * im
+
+
 def normalize(x):
     """Per-batch divide by max (utils/Helper_Functions.py:185-193), out of place."""
     B = x.shape[0]

@@ -33,6 +33,7 @@ EXPORTED = [
     "thz_radial_forward", "thz_radial_backward",
     "thz_gaussian_beam", "thz_thin_lens", "thz_aperture",
     "thz_intensity_mse_workspace_size", "thz_intensity_mse_forward", "thz_intensity_mse_backward",
+    "thz_resample_forward", "thz_resample_backward",
     "thz_fft_rows",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
@@ -125,6 +126,12 @@ class LossDesc(ctypes.Structure):
                 ("tB", ctypes.c_int), ("tC", ctypes.c_int)]
 
 
+class ResampleDesc(ctypes.Structure):
+    _fields_ = [("BC", ctypes.c_int), ("Hin", ctypes.c_int), ("Win", ctypes.c_int), ("Hout", ctypes.c_int),
+                ("Wout", ctypes.c_int), ("dx_in", ctypes.c_float), ("dy_in", ctypes.c_float),
+                ("dx_out", ctypes.c_float), ("dy_out", ctypes.c_float)]
+
+
 APERTURE_RECT, APERTURE_CIRC = 1, 2
 
 Q_FP, Q_STE, Q_PSQ, Q_SGV3, Q_NGS, Q_SGV1 = 0, 1, 2, 3, 4, 5
@@ -162,6 +169,8 @@ def _declare(lib):
                                               c_void_p]
     lib.thz_intensity_mse_backward.argtypes = [ctypes.POINTER(LossDesc), c_void_p, c_void_p, c_void_p, c_void_p,
                                                c_void_p, c_void_p]
+    lib.thz_resample_forward.argtypes = [ctypes.POINTER(ResampleDesc), c_void_p, c_void_p, c_void_p]
+    lib.thz_resample_backward.argtypes = [ctypes.POINTER(ResampleDesc), c_void_p, c_void_p, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]
     lib.thz_timing_reset.argtypes = []
     lib.thz_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]

@@ -209,6 +209,100 @@ __global__ void mse_backward_kernel(const float2* __restrict__ f, const float* _
   gf[q] = make_float2(2.f * dI * e.x, 2.f * dI * e.y);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Field_Resampler (Addons/Field_Resampler.py:19-118): bilinear grid_sample (zeros padding,
+// align_corners=True) of the complex field onto the centred output grid; adjoint by scatter.
+// ---------------------------------------------------------------------------------------------
+struct ResampleArgs {
+  int BC, Hin, Win, Hout, Wout;
+  float gx0, gx1, gy0, gy1;  // linspace(-((n-1)//2), (n-1)//2, n) end points of the output grid
+  float dxo, dyo, xnorm, ynorm;
+};
+
+struct Taps {
+  int x0, y0;
+  float w[4];  // nw, ne, sw, se
+};
+
+// torch grid_sampler_compute_source_index (align_corners) + the bilinear weights, fp32
+__device__ __forceinline__ Taps resample_taps(const ResampleArgs& a, int i, int j) {
+  const float gX = lin(a.gx0, a.gx1, a.Hout, i) * a.dxo;  // height coordinate of output row i
+  const float gY = lin(a.gy0, a.gy1, a.Wout, j) * a.dyo;  // width coordinate of output column j
+  const float gx = gY / a.ynorm, gy = gX / a.xnorm;       // grid[..., 0] (W), grid[..., 1] (H)
+  const float ix = ((gx + 1.0f) / 2.0f) * (float)(a.Win - 1);
+  const float iy = ((gy + 1.0f) / 2.0f) * (float)(a.Hin - 1);
+  const float fx = floorf(ix), fy = floorf(iy);
+  Taps t;
+  t.x0 = (int)fx;
+  t.y0 = (int)fy;
+  const float xe = fx + 1.0f, ye = fy + 1.0f;
+  t.w[0] = (xe - ix) * (ye - iy);
+  t.w[1] = (ix - fx) * (ye - iy);
+  t.w[2] = (xe - ix) * (iy - fy);
+  t.w[3] = (ix - fx) * (iy - fy);
+  if (!(ix == ix) || !(iy == iy)) t.x0 = t.y0 = -(1 << 30);  // NaN grid: every tap out of range
+  return t;
+}
+
+__global__ void resample_fwd(const float2* __restrict__ in, float2* __restrict__ out, ResampleArgs a) {
+  const int HWo = a.Hout * a.Wout;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HWo) return;
+  const int i = p / a.Wout, j = p - i * a.Wout;
+  const Taps t = resample_taps(a, i, j);
+  const int HWi = a.Hin * a.Win;
+  for (int bc = 0; bc < a.BC; ++bc) {
+    const float2* src = in + (size_t)bc * HWi;
+    float re = 0.f, im = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = t.x0 + (k & 1), y = t.y0 + (k >> 1);
+      if (x >= 0 && x < a.Win && y >= 0 && y < a.Hin) {
+        const float2 v = src[(size_t)y * a.Win + x];
+        re = re + v.x * t.w[k];
+        im = im + v.y * t.w[k];
+      }
+    }
+    out[(size_t)bc * HWo + p] = make_float2(re, im);
+  }
+}
+
+__global__ void resample_bwd(const float2* __restrict__ g, float2* __restrict__ gin, ResampleArgs a) {
+  const int HWo = a.Hout * a.Wout;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= HWo) return;
+  const int i = p / a.Wout, j = p - i * a.Wout;
+  const Taps t = resample_taps(a, i, j);
+  const int HWi = a.Hin * a.Win;
+  for (int bc = 0; bc < a.BC; ++bc) {
+    const float2 gv = g[(size_t)bc * HWo + p];
+    float* dst = reinterpret_cast<float*>(gin + (size_t)bc * HWi);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int x = t.x0 + (k & 1), y = t.y0 + (k >> 1);
+      if (x >= 0 && x < a.Win && y >= 0 && y < a.Hin) {
+        const size_t o = 2 * ((size_t)y * a.Win + x);
+        atomicAdd(dst + o, gv.x * t.w[k]);
+        atomicAdd(dst + o + 1, gv.y * t.w[k]);
+      }
+    }
+  }
+}
+
+static bool resample_args(const thz_resample_desc* d, ResampleArgs* a) {
+  if (!d || d->BC < 1 || d->Hin < 1 || d->Win < 1 || d->Hout < 1 || d->Wout < 1) return false;
+  a->BC = d->BC; a->Hin = d->Hin; a->Win = d->Win; a->Hout = d->Hout; a->Wout = d->Wout;
+  a->gx0 = (float)(-((d->Hout - 1) / 2));
+  a->gx1 = (float)((d->Hout - 1) / 2);
+  a->gy0 = (float)(-((d->Wout - 1) / 2));
+  a->gy1 = (float)((d->Wout - 1) / 2);
+  a->dxo = d->dx_out;
+  a->dyo = d->dy_out;
+  a->xnorm = d->dx_in * (float)((d->Hin - 1) / 2);  // dx * ((Hf - 1) // 2), fp32 (:82-85)
+  a->ynorm = d->dy_in * (float)((d->Win - 1) / 2);
+  return true;
+}
+
 static bool loss_args(const thz_loss_desc* d, LossArgs* a) {
   if (!d || d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1) return false;
   if (!(d->tB == 1 || d->tB == d->B) || !(d->tC == 1 || d->tC == d->C)) return false;
@@ -355,5 +449,30 @@ extern "C" int thz_intensity_mse_backward(const thz_loss_desc* d, const void* fi
                      (const float2*)field, target, stats, grad_loss, (float2*)grad_field, a, (float)(2.0 / n));
   THZ_LAUNCH_CHECK();
   kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_resample_forward(const thz_resample_desc* d, const void* in, void* out, thz_stream_t stream) {
+  ResampleArgs a;
+  if (!resample_args(d, &a) || !in || !out) return fail(THZ_E_ARG, "bad resample arguments");
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("resample_fwd", s);
+  const int n = d->Hout * d->Wout;
+  hipLaunchKernelGGL(resample_fwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_resample_backward(const thz_resample_desc* d, const void* grad_out, void* grad_in,
+                                     thz_stream_t stream) {
+  ResampleArgs a;
+  if (!resample_args(d, &a) || !grad_out || !grad_in) return fail(THZ_E_ARG, "bad resample arguments");
+  hipStream_t s = (hipStream_t)stream;
+  THZ_HIP_CHECK(hipMemsetAsync(grad_in, 0, sizeof(float2) * (size_t)d->BC * d->Hin * d->Win, s));
+  const int n = d->Hout * d->Wout;
+  hipLaunchKernelGGL(resample_bwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)grad_out,
+                     (float2*)grad_in, a);
+  THZ_LAUNCH_CHECK();
   return THZ_OK;
 }

@@ -150,3 +150,35 @@ def intensity_mse(field, target):
     if field.dtype != torch.complex64:
         raise TypeError(f"loss kernel computes in complex64 fields; got {field.dtype}")
     return _IntensityMSE.apply(field, target)
+
+
+class _Resample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, Hout, Wout, dx_in, dy_in, dx_out, dy_out):
+        _require_device(x, "field resampler")
+        x = x.contiguous()
+        B, C, H, W = x.shape
+        d = _lib.ResampleDesc(BC=B * C, Hin=H, Win=W, Hout=Hout, Wout=Wout, dx_in=dx_in, dy_in=dy_in, dx_out=dx_out,
+                              dy_out=dy_out)
+        out = torch.empty((B, C, Hout, Wout), dtype=x.dtype, device=x.device)
+        with torch.cuda.device(x.device):
+            _lib.check(_lib.lib().thz_resample_forward(ctypes.byref(d), _p(x), _p(out), _stream_handle()))
+        ctx.cfg = (d, (B, C, H, W))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        d, shape = ctx.cfg
+        g = g.contiguous()
+        gin = torch.empty(shape, dtype=g.dtype, device=g.device)
+        with torch.cuda.device(g.device):
+            _lib.check(_lib.lib().thz_resample_backward(ctypes.byref(d), _p(g), _p(gin), _stream_handle()))
+        return gin, None, None, None, None, None, None
+
+
+def resample(x, Hout, Wout, dx_in, dy_in, dx_out, dy_out):
+    """Bilinear resampling of [B, C, H, W] complex64 onto the centred (Hout, Wout) grid with the
+    output pixel pitch (Addons/Field_Resampler.py:74-118), differentiable."""
+    if x.dtype != torch.complex64:
+        raise TypeError(f"resampler kernel computes in complex64; got {x.dtype}")
+    return _Resample.apply(x, int(Hout), int(Wout), float(dx_in), float(dy_in), float(dx_out), float(dy_out))

@@ -583,13 +583,45 @@ def gen_donn(manifest):
     np.savez_compressed(os.path.join(HERE, "donn_golden.npz"), **arrays)
 
 
+def gen_addons(manifest):
+    """Addons: Field_Resampler (bilinear grid_sample onto a new grid) and Field_Cropper."""
+    FR = ref.import_module("Addons.Field_Resampler")
+    FC = ref.import_module("Addons.Field_Crop")
+    arrays = {}
+    manifest["addons"] = []
+    cases = [("rs_down", (1, 2, 64, 80), (0.5 * MM, 0.7 * MM), (48, 40), (0.6 * MM, 1.1 * MM)),
+             ("rs_up", (2, 1, 33, 47), (1.0 * MM, 1.0 * MM), (90, 64), (0.3 * MM, 0.55 * MM)),
+             ("rs_wide", (1, 1, 40, 40), (0.5 * MM, 0.5 * MM), (64, 64), (0.5 * MM, 0.5 * MM))]
+    for i, (name, shape, sp, oshape, osp) in enumerate(cases):
+        x = rand_field(shape, 50 + i)
+        g = rand_field((shape[0], shape[1]) + oshape, 60 + i)
+        wl = [C0 / 300e9] * shape[1] if shape[1] > 1 else C0 / 300e9
+        field = make_field(x, wl_arg([C0 / (300e9 + 10e9 * k) for k in range(shape[1])]), list(sp), False)
+        field._data = field._data.clone().requires_grad_(True)
+        rs = FR.Field_Resampler(oshape[0], oshape[1], osp[0], osp[1], device="cpu")
+        out = rs(field)
+        gx, = torch.autograd.grad(out.data, field._data, grad_outputs=torch.from_numpy(g))
+        arrays.update({f"{name}__in": x, f"{name}__gout": g, f"{name}__out32": out.data.detach().numpy(),
+                       f"{name}__gx32": gx.numpy()})
+        manifest["addons"].append(dict(name=name, kind="resample", shape=shape, spacing=sp, oshape=oshape,
+                                       ospacing=osp, f=[300 + 10 * k for k in range(shape[1])]))
+    x = rand_field((1, 1, 31, 50), 70)
+    field = make_field(x, C0 / 300e9, [MM, MM], False)
+    out = FC.Field_Cropper(20, 33)(field)
+    arrays.update({"crop__in": x, "crop__out32": out.data.numpy()})
+    manifest["addons"].append(dict(name="crop", kind="crop", oshape=[20, 33]))
+    np.savez_compressed(os.path.join(HERE, "addons_golden.npz"), **arrays)
+    print("addons", len(manifest["addons"]))
+
+
 def main():
     path = os.path.join(HERE, "manifest.json")
     if "--only" in sys.argv:
         which = sys.argv[sys.argv.index("--only") + 1]
         with open(path) as fh:
             manifest = json.load(fh)
-        {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat, "donn": gen_donn}[which](manifest)
+        {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat, "donn": gen_donn,
+         "addons": gen_addons}[which](manifest)
     else:
         manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
                     "asm": [], "czt": [], "rsc": [], "doe": []}
@@ -601,6 +633,7 @@ def main():
         gen_optics(manifest)
         gen_qat(manifest)
         gen_donn(manifest)
+        gen_addons(manifest)
     with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1, default=float)
 

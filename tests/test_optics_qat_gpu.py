@@ -232,3 +232,30 @@ def test_qat_graph_replay_matches_eager_with_fixed_noise():
         weights[graph] = system.doe.weight_init_phase.detach().cpu().numpy()
     np.testing.assert_allclose(losses[True], losses[False], rtol=1e-4)
     assert rel_l2(weights[True], weights[False]) <= 1e-4
+
+
+ADDONS = M.get("addons", [])
+
+
+@pytest.mark.parametrize("case", ADDONS, ids=[c["name"] for c in ADDONS])
+def test_addons_vs_golden(case):
+    from quantizationawarethzdoe_amd.Addons.Field_Crop import Field_Cropper
+    from quantizationawarethzdoe_amd.Addons.Field_Resampler import Field_Resampler
+    A = arrays("addons")
+    k = case["name"]
+    if case["kind"] == "crop":
+        f = _ef(A["crop__in"], [300], 1e-3, 1e-3)
+        out = Field_Cropper(*case["oshape"])(f)
+        np.testing.assert_array_equal(out.data.cpu().numpy(), A["crop__out32"])
+        return
+    f = _ef(A[f"{k}__in"], case["f"], *case["spacing"])
+    f.data.requires_grad_(True)
+    rs = Field_Resampler(case["oshape"][0], case["oshape"][1], case["ospacing"][0], case["ospacing"][1])
+    out = rs(f)
+    assert tuple(out.data.shape[-2:]) == tuple(case["oshape"])
+    # bilinear weights: torch's CPU grid_sample forms them in a differently rounded (vectorised)
+    # order, so parity is fp32-level (measured 2.3e-6 on rs_wide), bounded at 1e-5
+    assert rel_l2(out.data.detach().cpu().numpy(), A[f"{k}__out32"]) <= 1e-5
+    gx, = torch.autograd.grad(out.data, f.data, grad_outputs=torch.from_numpy(A[f"{k}__gout"]).to(_dev()))
+    assert rel_l2(gx.cpu().numpy(), A[f"{k}__gx32"]) <= 1e-5
+    assert out.spacing_host == [np.float32(case["ospacing"][0]), np.float32(case["ospacing"][1])]

@@ -301,3 +301,18 @@ def test_donn_oracle_matches_reference(case):
         orc.asm_forward(layer(i, inputs), lam, sp, 0.02, padding_scale=2)  # computed and discarded (nb :194)
     out = orc.asm_forward(layer(2, inputs), lam, sp, 0.05, padding_scale=2)
     assert rel_l2(out.numpy(), A[f"{k}__out32"]) <= 1e-5
+
+
+ADD = [c for c in M.get("addons", []) if c["kind"] == "resample"]
+
+
+@pytest.mark.parametrize("case", ADD, ids=[c["name"] for c in ADD])
+def test_resample_oracle_matches_reference(case):
+    A = arrays("addons")
+    k = case["name"]
+    x = torch.from_numpy(A[f"{k}__in"]).requires_grad_(True)
+    sp = torch.tensor(case["spacing"], dtype=torch.float32)
+    o = orc.resample(x, sp, case["oshape"][0], case["oshape"][1], case["ospacing"][0], case["ospacing"][1])
+    gx, = torch.autograd.grad(o, x, grad_outputs=torch.from_numpy(A[f"{k}__gout"]))
+    assert rel_l2(o.detach().numpy(), A[f"{k}__out32"]) <= 1e-6
+    assert rel_l2(gx.numpy(), A[f"{k}__gx32"]) <= 1e-6
