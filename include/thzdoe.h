@@ -120,6 +120,10 @@ typedef struct thz_rsc_desc {
   float dx, dy;
   float z;
   const float* wavelengths; /* host [C] */
+  int adjoint;              /* 1: the adjoint (autograd backward) of the scalar convolution:
+                               in [B, C, Ph - H, Pw - W] -> out [B, C, H, W], conj(FFT2(K)),
+                               windows exchanged; vectorial must be 0 (VRS backward applies it
+                               per plane and folds the Ez chain on the host side) */
 } thz_rsc_desc;
 
 int thz_rsc_workspace_size(const thz_rsc_desc* d, size_t* bytes);

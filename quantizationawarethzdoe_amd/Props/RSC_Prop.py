@@ -102,10 +102,28 @@ class VRS_prop(RSC_prop):
 
 
 class _RscFunction(torch.autograd.Function):
+    """Forward on the HIP convolution; backward = the adjoint convolution (conj FFT2(K), windows
+    exchanged).  VRS: out = [RSC(Ex), RSC(Ey), RSC(Ez)], Ez = Ex x/r + Ey y/r, so
+    dEx = RSC^H(g0) + x/r RSC^H(g2) and dEy = RSC^H(g1) + y/r RSC^H(g2) on the unpadded grid."""
+
     @staticmethod
     def forward(ctx, data, wavelengths, spacing, z, vectorial):
+        ctx.cfg = (wavelengths, spacing, z, vectorial, tuple(data.shape))
         return _prop.rsc_apply(data, wavelengths, spacing, z, vectorial)
 
     @staticmethod
     def backward(ctx, g):
-        raise NotImplementedError("RSC_prop backward is not implemented on the MI355X path yet")
+        wavelengths, spacing, z, vectorial, shape = ctx.cfg
+        B, C, H, W = shape
+        adj = _prop.rsc_apply(g.contiguous(), wavelengths, spacing, z, adjoint=True, field_hw=(H, W))
+        if not vectorial:
+            return adj, None, None, None, None
+        dx = torch.tensor(spacing[0], dtype=torch.float32)
+        x = torch.linspace(float(-dx * H / 2), float(dx * H / 2), H, device=g.device)
+        y = torch.linspace(float(-dx * W / 2), float(dx * W / 2), W, device=g.device)
+        X, Y = torch.meshgrid(x, y, indexing="ij")
+        r = torch.sqrt(X ** 2 + Y ** 2 + torch.tensor(z, dtype=torch.float32) ** 2)
+        gin = torch.zeros(shape, dtype=adj.dtype, device=g.device)
+        gin[0] = adj[0] + adj[2] * (X / r)
+        gin[1] = adj[1] + adj[2] * (Y / r)
+        return gin, None, None, None, None

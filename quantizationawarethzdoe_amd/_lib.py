@@ -71,7 +71,7 @@ class RscDesc(ctypes.Structure):
     _fields_ = [
         ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
         ("vectorial", ctypes.c_int), ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("z", ctypes.c_float),
-        ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+        ("wavelengths", ctypes.POINTER(ctypes.c_float)), ("adjoint", ctypes.c_int),
     ]
 
 

@@ -232,7 +232,10 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
-      auto ld1 = [&](int m, int r, int idx) { return cmul(sp[m][r], tcol[idx]); };
+      auto ld1 = [&](int m, int r, int idx) {
+        const float2 t = tcol[idx];
+        return cmul(sp[m][r], a.adjoint ? make_float2(t.x, -t.y) : t);
+      };
       float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
@@ -314,7 +317,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       for (int m = 0; m < FFT_MAXV; ++m) {
         const int i = tm + m * nt;
         if (i < Ph)
-          lds[padx(i)] = cmul(sp[m], tcol ? tcol[i] : tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky));
+          lds[padx(i)] = cmul(sp[m], tcol ? (a.adjoint ? make_float2(tcol[i].x, -tcol[i].y) : tcol[i])
+                                          : tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky));
       }
       __syncthreads();
       fft_lds<true>(lds, ph, tm, nt);
@@ -736,10 +740,11 @@ static int rsc_plan(const thz_rsc_desc* d, RscPlan* p) {
   g.Pw = d->W + 2 * (d->W / 2);
   if (g.Ph > FFT_MAX_N || g.Pw > FFT_MAX_N) return fail(THZ_E_UNSUPPORTED, "RSC grid %dx%d too large", g.Ph, g.Pw);
   g.BC = (d->vectorial ? 3 : d->B) * d->C;
-  g.Hin = d->H;
-  g.Win = d->W;
-  g.Hout = g.Ph - d->H;  // ifft2(...)[..., H:, W:] (:207)
-  g.Wout = g.Pw - d->W;
+  if (d->adjoint && d->vectorial) return fail(THZ_E_ARG, "RSC adjoint is per plane: vectorial must be 0");
+  g.Hin = d->adjoint ? g.Ph - d->H : d->H;
+  g.Win = d->adjoint ? g.Pw - d->W : d->W;
+  g.Hout = d->adjoint ? d->H : g.Ph - d->H;  // ifft2(...)[..., H:, W:] (:207)
+  g.Wout = d->adjoint ? d->W : g.Pw - d->W;
   g.ncols = g.Pw;
   g.J = g.Pw / 2;
   g.ncb = (g.ncols + CB - 1) / CB;
@@ -805,8 +810,14 @@ extern "C" int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out,
   a.C = d->C;
   a.Ph = g.Ph;
   a.Pw = g.Pw;
-  a.in_r0 = 0; a.in_c0 = 0; a.Hin = d->H; a.Win = d->W;         // U[..., :H, :W] = field (:198-200)
-  a.out_r0 = d->H; a.out_c0 = d->W; a.Hout = g.Hout; a.Wout = g.Wout;
+  if (!d->adjoint) {
+    a.in_r0 = 0; a.in_c0 = 0; a.Hin = d->H; a.Win = d->W;         // U[..., :H, :W] = field (:198-200)
+    a.out_r0 = d->H; a.out_c0 = d->W; a.Hout = g.Hout; a.Wout = g.Wout;
+  } else {  // adjoint: gradient placed at [H:, W:], result read back from [:H, :W]
+    a.in_r0 = d->H; a.in_c0 = d->W; a.Hin = g.Hin; a.Win = g.Win;
+    a.out_r0 = 0; a.out_c0 = 0; a.Hout = g.Hout; a.Wout = g.Wout;
+    a.adjoint = 1;
+  }
   a.ncols = g.ncols;
   a.ncb = g.ncb;
   a.ncbu = g.ncbu;

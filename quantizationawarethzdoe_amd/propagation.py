@@ -150,25 +150,34 @@ def czt_apply(data, wavelengths, spacing, z, outH, outW, odx, ody):
     return out
 
 
-def rsc_apply(data, wavelengths, spacing, z, vectorial=False):
+def rsc_apply(data, wavelengths, spacing, z, vectorial=False, adjoint=False, field_hw=None):
     """Rayleigh-Sommerfeld convolution (Props/RSC_Prop.py:170-321) on the HIP kernels.
 
     [B,C,H,W] -> [Bo,C,Ph-H,Pw-W], Ph = H + 2 floor(H/2); vectorial: Ex/Ey planes in, 3 planes out.
+    adjoint: the autograd backward of the scalar convolution, [B,C,Ph-H,Pw-W] -> [B,C,H,W] with
+    (H, W) = field_hw, the forward field's shape.
     """
     _require_device(data, "RSC")
     if data.dtype != torch.complex64:
         raise TypeError(f"RSC kernels compute in complex64; got {data.dtype}")
     data = data.contiguous()
-    B, C, H, W = data.shape
+    B, C = data.shape[:2]
+    H, W = field_hw if adjoint else data.shape[-2:]
     wl = _lib.float_array(wavelengths)
-    d = _lib.RscDesc(B=B, C=C, H=H, W=W, vectorial=int(bool(vectorial)), dx=float(spacing[0]),
-                     dy=float(spacing[1]), z=float(z), wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)))
+    d = _lib.RscDesc(B=B, C=C, H=int(H), W=int(W), vectorial=int(bool(vectorial)), dx=float(spacing[0]),
+                     dy=float(spacing[1]), z=float(z), wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
+                     adjoint=int(bool(adjoint)))
     L = _lib.lib()
     nbytes = ctypes.c_size_t(0)
     _lib.check(L.thz_rsc_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
     ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
-    Bo = 3 if vectorial else B
-    out = torch.empty((Bo, C, 2 * (H // 2), 2 * (W // 2)), dtype=torch.complex64, device=data.device)
+    if adjoint:
+        if tuple(data.shape[-2:]) != (2 * (H // 2), 2 * (W // 2)):
+            raise ValueError(f"RSC adjoint: gradient {tuple(data.shape)} does not match field {(H, W)}")
+        out = torch.empty((B, C, int(H), int(W)), dtype=torch.complex64, device=data.device)
+    else:
+        Bo = 3 if vectorial else B
+        out = torch.empty((Bo, C, 2 * (H // 2), 2 * (W // 2)), dtype=torch.complex64, device=data.device)
     with torch.cuda.device(data.device):
         _lib.check(L.thz_rsc_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
