@@ -100,6 +100,8 @@ typedef struct thz_czt_desc {
   float odx, ody;
   float z;
   const float* wavelengths; /* host [C] */
+  int adjoint;              /* 1: the adjoint (autograd backward): in [B, C, outW, outH] ->
+                               out [B, C, H, W]; conj chirps / filter / RS kernels, passes reversed */
 } thz_czt_desc;
 
 int thz_czt_workspace_size(const thz_czt_desc* d, size_t* bytes);

@@ -7,7 +7,8 @@ defaults (output grid = input grid, :280-290) returning a new ElectricField with
 reference's [B, C, outW, outH] (square outputs only, as the reference's F0 broadcast at :248
 requires; a non-square request raises).  The per-call debug prints of the reference
 (:167-176, :217) are not reproduced.  The math runs in libthzdoe's gfx950 kernels
-(thz_czt.hip), with the chirp tables generated in double precision on the device.
+(thz_czt.hip), with the chirp tables generated in double precision on the device; backward runs
+the adjoint kernels.
 """
 from __future__ import annotations
 
@@ -71,13 +72,20 @@ class CZT_prop(nn.Module):
 
 
 class _CztFunction(torch.autograd.Function):
+    """Forward and adjoint (conjugated chirps, filter and RS kernels, passes reversed) on the
+    HIP Bluestein kernels."""
+
     @staticmethod
     def forward(ctx, data, wavelengths, spacing, z, outH, outW, odx, ody):
+        ctx.cfg = (wavelengths, spacing, z, outH, outW, odx, ody, tuple(data.shape))
         return _prop.czt_apply(data, wavelengths, spacing, z, outH, outW, odx, ody)
 
     @staticmethod
     def backward(ctx, g):
-        raise NotImplementedError("CZT_prop backward is not implemented on the MI355X path yet")
+        wavelengths, spacing, z, outH, outW, odx, ody, shape = ctx.cfg
+        gin = _prop.czt_apply(g.contiguous(), wavelengths, spacing, z, outH, outW, odx, ody, adjoint=True,
+                              field_hw=shape[-2:])
+        return gin, None, None, None, None, None, None, None
 
 
 class VCZT_prop(CZT_prop):

@@ -63,7 +63,7 @@ class CztDesc(ctypes.Structure):
         ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
         ("outH", ctypes.c_int), ("outW", ctypes.c_int),
         ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("odx", ctypes.c_float), ("ody", ctypes.c_float),
-        ("z", ctypes.c_float), ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+        ("z", ctypes.c_float), ("wavelengths", ctypes.POINTER(ctypes.c_float)), ("adjoint", ctypes.c_int),
     ]
 
 

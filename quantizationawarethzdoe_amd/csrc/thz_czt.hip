@@ -218,6 +218,113 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
 }
 
 // ---------------------------------------------------------------------------------------------
+// Adjoint (autograd backward).  Per pass the forward is y[q] = post[q] sum_w x[w] pre[w]
+// g[(q + m - w) mod N] (N = np2, post holding the unnormalised IFFT's 1/N), so
+//   x^[w] = conj(pre[w]) IFFT_N( FFT_N(Z) conj(FFT_N(g)) )[w],  Z[(q + m) mod N] = conj(post[q]) y^[q]
+// i.e. the same kernel shape with the conj filter spectrum and the windows exchanged; the
+// passes run in reverse order (columns first), F0 / the RS input kernel conjugated at the ends.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float2 conjf2(float2 v) { return make_float2(v.x, -v.y); }
+
+// one Bluestein transform of the adjoint in an LDS workgroup: loader / storer on N points
+template <int PN, class LdX, class StY>
+__device__ __forceinline__ void czt_adj_line(float2* lds, const FftPlan& pl, const float2* __restrict__ ft,
+                                             LdX& load_x, StY& store_y) {
+  int tid = threadIdx.x;
+  if constexpr (PN > 0) {
+    using S = Pow2Sched<PN>;
+    constexpr int TT = CztGeo<PN>::T;
+    constexpr int RL = S::radix(S::NST - 1, false);
+    constexpr int MBL = PN / RL / TT;
+    float2 sp[MBL][RL];
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pl.tw, tid, blockDim.x);
+    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
+    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
+    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
+    asm volatile("" : "+v"(tid));
+    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], conjf2(ft[idx])); };
+    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
+    fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tid, ld1, sv1);
+  } else {
+    const int n = pl.n, nt = blockDim.x;
+    for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
+    __syncthreads();
+    fft_lds<false>(lds, pl, tid, nt);
+    for (int j = tid; j < n; j += nt) lds[padx(j)] = cmul(lds[padx(j)], conjf2(ft[j]));
+    __syncthreads();
+    fft_lds<true>(lds, pl, tid, nt);
+    for (int j = tid; j < n; j += nt) store_y(j, lds[padx(j)]);
+  }
+}
+
+// adjoint of pass B: G [BC][outW][outH] (column q) -> V^ blocked [BC][q/16][h][16]
+template <int PN>
+__global__ void __launch_bounds__(1024) czt_cols_adj(const float2* __restrict__ G, float2* __restrict__ V,
+                                                    const float2* __restrict__ ws, FftPlan pl, CztArgs a) {
+  extern __shared__ float2 lds[];
+  const int id = xcd_chunk(blockIdx.x, gridDim.x);
+  const int bc = id / a.outH, q = id - bc * a.outH;
+  const int c = bc % a.C;
+  const float lam = a.lam[c];
+  const float k = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, a.z);
+  const float2* pre = ws + a.preB + (size_t)c * a.tabStride;
+  const float2* post = ws + a.postB + (size_t)c * a.tabStride;
+  const float2* ft = ws + a.ftB + (size_t)c * a.tabStride;
+  const float2* src = G + (size_t)bc * a.outW * a.outH + q;
+  float2* dst = V + (size_t)bc * a.ncbA * CB * a.H + blk(q, 0, a.H);
+  const int m = a.H, M = a.outW, N = pl.n;
+  const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
+  const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
+  const float cst = ((a.z * a.odx) * a.ody) * lam;
+  auto load_x = [&](int j) {
+    int p = j - m;
+    if (p < 0) p += N;
+    if (p >= M) return make_float2(0.f, 0.f);
+    const float2 F0 = rs_kernel(lin(xlo, xhi, a.outH, p), yq, a.z, k, rph);
+    return cmul(conjf2(post[p]), cscale(cmul(conjf2(F0), src[(size_t)p * a.outH]), cst));
+  };
+  auto store_y = [&](int j, float2 v) {
+    if (j < m) dst[(size_t)j * CB] = cmul(conjf2(pre[j]), v);
+  };
+  czt_adj_line<PN>(lds, pl, ft, load_x, store_y);
+}
+
+// adjoint of pass A: V^ row h -> grad_in [BC][H][W]
+template <int PN>
+__global__ void __launch_bounds__(1024) czt_rows_adj(const float2* __restrict__ V, float2* __restrict__ gin,
+                                                    const float2* __restrict__ ws, FftPlan pl, CztArgs a) {
+  extern __shared__ float2 lds[];
+  const int row = blockIdx.x;
+  const int bc = row / a.H, h = row - bc * a.H;
+  const int c = bc % a.C;
+  const float lam = a.lam[c];
+  const float k = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, a.z);
+  const float xh = lin(-(float)a.H * a.dx / 2.0f, (float)a.H * a.dx / 2.0f, a.H, h);
+  const float2* pre = ws + a.preA + (size_t)c * a.tabStride;
+  const float2* post = ws + a.postA + (size_t)c * a.tabStride;
+  const float2* ft = ws + a.ftA + (size_t)c * a.tabStride;
+  const float2* src = V + (size_t)bc * a.ncbA * CB * a.H;
+  float2* dst = gin + ((size_t)bc * a.H + h) * a.W;
+  const int m = a.W, M = a.outH, N = pl.n;
+  const float ylo = -(float)a.W * a.dy / 2.0f, yhi = (float)a.W * a.dy / 2.0f;
+  auto load_x = [&](int j) {
+    int qq = j - m;
+    if (qq < 0) qq += N;
+    if (qq >= M) return make_float2(0.f, 0.f);
+    return cmul(conjf2(post[qq]), src[blk(qq, h, a.H)]);
+  };
+  auto store_y = [&](int j, float2 v) {
+    if (j < m) {
+      const float2 F = rs_kernel(xh, lin(ylo, yhi, a.W, j), a.z, k, rph);
+      dst[j] = cmul(conjf2(F), cmul(conjf2(pre[j]), v));
+    }
+  };
+  czt_adj_line<PN>(lds, pl, ft, load_x, store_y);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------------------
 static int np2_of(int x) {
@@ -318,7 +425,11 @@ static int czt_lds_attr() {
         (const void*)czt_rows<0>,     (const void*)czt_rows<1024>, (const void*)czt_rows<2048>,
         (const void*)czt_rows<4096>,  (const void*)czt_rows<8192>, (const void*)czt_rows<16384>,
         (const void*)czt_cols<0>,     (const void*)czt_cols<1024>, (const void*)czt_cols<2048>,
-        (const void*)czt_cols<4096>,  (const void*)czt_cols<8192>, (const void*)czt_cols<16384>};
+        (const void*)czt_cols<4096>,  (const void*)czt_cols<8192>, (const void*)czt_cols<16384>,
+        (const void*)czt_rows_adj<0>,  (const void*)czt_rows_adj<1024>, (const void*)czt_rows_adj<2048>,
+        (const void*)czt_rows_adj<4096>, (const void*)czt_rows_adj<8192>, (const void*)czt_rows_adj<16384>,
+        (const void*)czt_cols_adj<0>,  (const void*)czt_cols_adj<1024>, (const void*)czt_cols_adj<2048>,
+        (const void*)czt_cols_adj<4096>, (const void*)czt_cols_adj<8192>, (const void*)czt_cols_adj<16384>};
     for (const void* k : ks) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       if (e != hipSuccess) err = e;
@@ -377,6 +488,17 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
     if ((e = thz_fft_rows(ws + a.ftB + (size_t)c * a.tabStride, ws + a.ftB + (size_t)c * a.tabStride, 1,
                           a.pb.np2, 0, stream)))
       return e;
+  }
+  if (d->adjoint) {  // G [B, C, outW, outH] -> grad_in [B, C, H, W]: column pass first
+    KernelTimer kt("czt_adjoint", s);
+    THZ_CZT_SWITCH(a.pb.np2, czt_cols_adj, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
+                   fft_lds_bytes(a.pb.np2), s, (const float2*)in, V, (const float2*)ws, plB, a);
+    THZ_LAUNCH_CHECK();
+    THZ_CZT_SWITCH(a.pa.np2, czt_rows_adj, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
+                   fft_lds_bytes(a.pa.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plA, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+    return THZ_OK;
   }
   {
     KernelTimer kt("czt_rows", s);

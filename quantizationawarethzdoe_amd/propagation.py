@@ -127,22 +127,28 @@ def fft_rows(x, inverse=False):
     return out
 
 
-def czt_apply(data, wavelengths, spacing, z, outH, outW, odx, ody):
-    """Chirp-z propagation [B,C,H,W] -> [B,C,outW,outH] (Props/CZT_Prop.py:252-314) on the HIP kernels."""
+def czt_apply(data, wavelengths, spacing, z, outH, outW, odx, ody, adjoint=False, field_hw=None):
+    """Chirp-z propagation [B,C,H,W] -> [B,C,outW,outH] (Props/CZT_Prop.py:252-314) on the HIP kernels.
+
+    adjoint: the autograd backward, [B,C,outW,outH] -> [B,C,H,W] with (H, W) = field_hw."""
     _require_device(data, "CZT")
     if data.dtype != torch.complex64:
         raise TypeError(f"CZT kernels compute in complex64; got {data.dtype}")
     data = data.contiguous()
-    B, C, H, W = data.shape
+    B, C = data.shape[:2]
+    H, W = (int(v) for v in (field_hw if adjoint else data.shape[-2:]))
+    if adjoint and tuple(data.shape[-2:]) != (int(outW), int(outH)):
+        raise ValueError(f"CZT adjoint: gradient {tuple(data.shape)} is not [B, C, outW, outH]")
     wl = _lib.float_array(wavelengths)
     d = _lib.CztDesc(B=B, C=C, H=H, W=W, outH=int(outH), outW=int(outW), dx=float(spacing[0]),
                      dy=float(spacing[1]), odx=float(odx), ody=float(ody), z=float(z),
-                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)))
+                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)), adjoint=int(bool(adjoint)))
     L = _lib.lib()
     nbytes = ctypes.c_size_t(0)
     _lib.check(L.thz_czt_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
     ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
-    out = torch.empty((B, C, int(outW), int(outH)), dtype=torch.complex64, device=data.device)
+    oshape = (B, C, H, W) if adjoint else (B, C, int(outW), int(outH))
+    out = torch.empty(oshape, dtype=torch.complex64, device=data.device)
     with torch.cuda.device(data.device):
         _lib.check(L.thz_czt_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),

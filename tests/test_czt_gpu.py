@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 import torch
 
-from tests.golden_io import arrays, manifest, rel_l2
+from oracle import thz_oracle as orc
+from tests.golden_io import arrays, manifest, rel_l2, wavelengths
 
 pytestmark = pytest.mark.gpu
 M = manifest()
@@ -39,3 +40,33 @@ def test_czt_rejects_non_square_output():
     x = torch.zeros(1, 1, 32, 32, dtype=torch.complex64, device="cuda:0")
     with pytest.raises(RuntimeError, match="square"):
         P.czt_apply(x, [1e-3], [1e-3, 1e-3], 0.1, 16, 8, 1e-3, 1e-3)
+
+
+@pytest.mark.parametrize("H,W,out,C", [(48, 64, 24, 2), (64, 64, 16, 1), (40, 36, 40, 1)])
+def test_czt_backward_vs_oracle_autograd(H, W, out, C):
+    """CZT_prop backward (adjoint Bluestein kernels) vs autograd through the fp64 oracle."""
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.CZT_Prop import CZT_prop
+    rng = np.random.default_rng(H + W + out)
+    x = (rng.standard_normal((1, C, H, W)) + 1j * rng.standard_normal((1, C, H, W))).astype(np.complex64)
+    freqs = [280 + 30 * c for c in range(C)]
+    wl = [C0 / (f * 1e9) for f in freqs]
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(x).to(dev).requires_grad_(True)
+    field = ElectricField(xd, wavelengths=wl if C > 1 else wl[0], spacing=[0.5e-3, 0.6e-3], device=dev)
+    o = CZT_prop(z_distance=0.2, device=dev)(field, out, out, 0.35e-3, 0.35e-3).data
+    g = (rng.standard_normal(o.shape) + 1j * rng.standard_normal(o.shape)).astype(np.complex64)
+    gx, = torch.autograd.grad(o, xd, grad_outputs=torch.from_numpy(g).to(dev))
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        xo = torch.from_numpy(x).to(torch.complex128).requires_grad_(True)
+        sp = torch.tensor([0.5e-3, 0.6e-3], dtype=torch.float32).double()
+        ro = orc.czt_forward(xo, wavelengths(freqs, True), sp, 0.2, out, out,
+                             float(torch.tensor(0.35e-3, dtype=torch.float32)),
+                             float(torch.tensor(0.35e-3, dtype=torch.float32)))
+        ro_g, = torch.autograd.grad(ro, xo, grad_outputs=torch.from_numpy(g).to(torch.complex128))
+    finally:
+        torch.set_default_dtype(old)
+    assert gx.shape == xd.shape
+    assert rel_l2(gx.cpu().numpy(), ro_g.numpy()) <= 1e-3, rel_l2(gx.cpu().numpy(), ro_g.numpy())
