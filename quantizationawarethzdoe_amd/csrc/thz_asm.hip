@@ -20,6 +20,8 @@
 // The adjoint (autograd backward) is the same pipeline with conj(H) and the input and
 // output windows exchanged.
 #include <algorithm>
+#include <map>
+#include <mutex>
 #include <cmath>
 #include <mutex>
 #include <vector>
@@ -40,6 +42,7 @@ struct AsmArgs {
   int ncb;                        // column blocks of CB columns (blocked T layout)
   int ncbu;                       // column blocks of CBU columns (blocked U layout)
   int nz, zoff;                   // z-planes in this chunk, offset into zv
+  int kfull, kparts;              // K2 tasks: kfull whole columns, then the rest split in kparts z-ranges
   int bl, adjoint;
   float dx, dy, scale;
   const float2* tft;  // RSC: column-major transfer-function table [C][ncols][Ph] (nullptr: analytic ASM)
@@ -201,7 +204,18 @@ template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   extern __shared__ float2 lds[];
-  const int id = xcd_chunk(blockIdx.x, gridDim.x);
+  // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
+  // resident-workgroup count), the last partial round's columns are split into kparts z-ranges
+  // so that round is short instead of a whole column pass on a few CUs.
+  int id, z_lo = 0, z_hi = a.nz;
+  if ((int)blockIdx.x < a.kfull) {
+    id = xcd_chunk(blockIdx.x, a.kfull);
+  } else {
+    const int t = blockIdx.x - a.kfull, part = t % a.kparts;
+    id = a.kfull + t / a.kparts;
+    z_lo = part * a.nz / a.kparts;
+    z_hi = (part + 1) * a.nz / a.kparts;
+  }
   const int bc = id / a.ncols, c = id - bc * a.ncols;
   const int nt = blockDim.x;
   const int Ph = a.Ph;
@@ -253,8 +267,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
     const float kl = TWO_PI_F / lam;
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
-    if ((int)threadIdx.x < a.nz) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + threadIdx.x]);
+    if ((int)threadIdx.x < z_hi - z_lo) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + threadIdx.x]);
       int lo = -1, hi = PN / 2 + 1;
       const int bl = a.bl, P = a.Ph;
       const float dx = a.dx;
@@ -269,9 +283,9 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       mz[threadIdx.x] = lo;
     }
     __syncthreads();  // mz visible
-    for (int zz = 0; zz < a.nz; ++zz) {
+    for (int zz = z_lo; zz < z_hi; ++zz) {
       const float z = a.zv[a.zoff + zz];
-      const int M = mz[zz];
+      const int M = mz[zz - z_lo];
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
@@ -308,7 +322,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       sp[m] = i < Ph ? lds[padx(i)] : make_float2(0.f, 0.f);
     }
     const float2* tcol = a.tft ? a.tft + ((size_t)(bc % a.C) * a.ncols + c) * Ph : nullptr;
-    for (int zz = 0; zz < a.nz; ++zz) {
+    for (int zz = z_lo; zz < z_hi; ++zz) {
       const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
       int tm = threadIdx.x;
       asm volatile("" : "+v"(tm));
@@ -598,6 +612,49 @@ static int ensure_lds_attr() {
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Workgroups of the column pass resident on the whole device at once (CUs x occupancy).
+static int k2_resident(int Ph, int threads, size_t lds) {
+  static std::mutex mu;
+  static std::map<std::pair<int, int>, int> cache;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  std::lock_guard<std::mutex> lk(mu);
+  auto key = std::make_pair(dev, Ph);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const void* k = nullptr;
+  switch (pow2_kind(Ph)) {
+    case 1024: k = (const void*)asm_cols<1024>; break;
+    case 2048: k = (const void*)asm_cols<2048>; break;
+    case 4096: k = (const void*)asm_cols<4096>; break;
+    case 8192: k = (const void*)asm_cols<8192>; break;
+    case 16384: k = (const void*)asm_cols<16384>; break;
+    default: k = (const void*)asm_cols<0>; break;
+  }
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    per_cu = cus = 0;
+  const int r = per_cu * cus;
+  cache[key] = r;
+  return r;
+}
+
+// K2 task split: whole columns for the full dispatch rounds, the remainder split by z-range.
+static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds) {
+  const int nc = g.ncols * g.BC;
+  const int G = k2_resident(g.Ph, threads, lds);
+  if (G <= 0 || a->nz <= 1) {
+    a->kfull = nc;
+    a->kparts = 1;
+    return nc;
+  }
+  const int full = nc / G * G, rem = nc - full;
+  a->kfull = full;
+  a->kparts = rem ? std::max(1, std::min(a->nz, G / rem)) : 1;
+  return full + rem * a->kparts;
+}
+
 static size_t ws_bytes(const AsmGeom& g) {
   return align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)) +
          align256((size_t)g.zc * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2));
@@ -621,8 +678,9 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     a.nz = std::min(g.zc, Z - z0);
     {
       KernelTimer kt("asm_cols", s);
-      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(g.ncols * g.BC), dim3(th), fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z, s,
-                      (const float2*)T, U, ph, a);
+      const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+      const int ntask = k2_tasks(g, &a, th, lds2);
+      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       THZ_LAUNCH_CHECK();
       kt.stop();
     }
