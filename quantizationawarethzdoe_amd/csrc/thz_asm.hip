@@ -134,7 +134,7 @@ __device__ __forceinline__ float2 tf_value(const AsmArgs& a, const TfScalars& s,
 // plan, data staged through LDS.
 template <int PN>
 struct Geo {
-  static constexpr int T = PN > 0 ? PN / FFT_MAXV : 0;
+  static constexpr int T = PN > 0 ? PN / pow2_v(PN) : 0;
 };
 
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
@@ -200,8 +200,11 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
 // ---------------------------------------------------------------------------------------------
 // K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
 // ---------------------------------------------------------------------------------------------
+#ifndef THZ_K2_WPE
+#define THZ_K2_WPE 1
+#endif
 template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K2_WPE))) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   extern __shared__ float2 lds[];
   // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
@@ -360,7 +363,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
     // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
     // frequencies), a multiple of CBU: the blocked address is then base(c0) + delta_q*Hout,
     // one add per element instead of the full blk_u() per element.
-    constexpr int NB0 = PN / 16;
+    constexpr int NB0 = PN / pow2_v(PN);  // first stage: radix pow2_v, L = 1
     static_assert(NB0 % CBU == 0, "band offsets must be whole U blocks");
     static_assert(Geo<PN>::T == NB0, "one first-stage butterfly per thread: i = tid");
     const int c0 = tid + a.J;
@@ -549,11 +552,11 @@ static void geometry(const thz_asm_desc* d, AsmGeom* g) {
   g->ncbu = (g->ncols + CBU - 1) / CBU;
   int zc = d->z_chunk > 0 ? d->z_chunk : 0;
   if (zc == 0) {
-    // default: up to 16 z-planes per column pass (the forward column FFT and the T read are
-    // shared by the chunk), U capped at 2.5 GiB of the 288 GB HBM.  Measured on cfg2:
-    // z_chunk 1/4/8/16 -> 2006/2620/2753/2859 planes/s.
+    // default: up to 32 z-planes per column pass (the forward column FFT and the T read are
+    // shared by the chunk), U capped at 5 GiB of the 288 GB HBM.  Measured on cfg2 (current
+    // kernels, 64 planes): z_chunk 16/32/64 -> 5925/6069/6113 planes/s.
     const double per_z = (double)g->BC * g->ncbu * CBU * g->Hout * sizeof(float2);
-    zc = (int)std::max(1.0, std::min(16.0, std::floor((2560.0 * 1024 * 1024) / per_z)));
+    zc = (int)std::max(1.0, std::min(32.0, std::floor((5120.0 * 1024 * 1024) / per_z)));
   }
   g->zc = std::min(zc, d->adjoint ? 1 : d->Z);
 }
@@ -565,7 +568,7 @@ static int pow2_kind(int n) {
     default: return 0;
   }
 }
-static int threads_for(int n) { return pow2_kind(n) ? n / FFT_MAXV : fft_threads(n); }
+static int threads_for(int n) { return pow2_kind(n) ? n / pow2_v(n) : fft_threads(n); }
 
 #define THZ_POW2_SWITCH(n, KER, ...)                                                              \
   switch (pow2_kind(n)) {                                                                          \

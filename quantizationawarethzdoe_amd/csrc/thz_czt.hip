@@ -99,7 +99,7 @@ __global__ void czt_tables(CztArgs a, float2* __restrict__ ws, int pass) {
 
 template <int PN>
 struct CztGeo {
-  static constexpr int T = PN > 0 ? PN / FFT_MAXV : 0;
+  static constexpr int T = PN > 0 ? PN / pow2_v(PN) : 0;
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -439,7 +439,7 @@ static int czt_lds_attr() {
   return THZ_OK;
 }
 
-static int threads_pow2_or(int n) { return czt_pow2(n) ? n / FFT_MAXV : fft_threads(n); }
+static int threads_pow2_or(int n) { return czt_pow2(n) ? n / pow2_v(n) : fft_threads(n); }
 
 }  // namespace thz
 

@@ -24,6 +24,13 @@ namespace thz {
 
 constexpr int FFT_MAX_STAGES = 24;
 constexpr int FFT_MAXV = 16;  // complex values held per thread per stage (N <= 16 * threads)
+#ifndef THZ_PV
+#define THZ_PV 16
+#endif
+// Power-of-two path: values (= largest radix) per thread, THZ_PV where N / THZ_PV threads fit
+// one workgroup (1024), else 16.  T = N / pow2_v(N) threads per transform.
+__host__ __device__ constexpr int pow2_v(int n) { return n / THZ_PV <= 1024 ? THZ_PV : 16; }
+constexpr int pow2_log(int v) { return v <= 1 ? 0 : 1 + pow2_log(v >> 1); }
 
 struct FftPlan {
   int n;                       // transform length
@@ -425,13 +432,15 @@ struct Pow2Sched {
     return l;
   }
   static constexpr int LOG = log2n();
-  static constexpr int NS16 = LOG / 4;
-  static constexpr int REM = 1 << (LOG % 4);
+  static constexpr int V = pow2_v(N);
+  static constexpr int LV = pow2_log(V);
+  static constexpr int NS16 = LOG / LV;  // full-radix (V) stages
+  static constexpr int REM = 1 << (LOG % LV);
   static constexpr int NST = NS16 + (REM > 1 ? 1 : 0);
   static constexpr int radix(int s, bool small_first) {
-    if (REM == 1) return 16;
-    if (small_first) return s == 0 ? REM : 16;
-    return s == NST - 1 ? REM : 16;
+    if (REM == 1) return V;
+    if (small_first) return s == 0 ? REM : V;
+    return s == NST - 1 ? REM : V;
   }
 };
 
