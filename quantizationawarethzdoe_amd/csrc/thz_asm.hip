@@ -245,6 +245,14 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
     fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tid, ld0, sv0);
+    if (!a.tft) {
+      // 1 / (Ph Pw) is a power of two: scaling the spectrum once per column instead of every
+      // output plane is exact
+#pragma unroll
+      for (int m = 0; m < MBL; ++m)
+#pragma unroll
+        for (int r = 0; r < RL; ++r) sp[m][r] = cscale(sp[m][r], a.scale);
+    }
     if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
       int tz = threadIdx.x;
@@ -285,6 +293,16 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
       }
       mz[threadIdx.x] = lo;
     }
+    // sqrt(k^2 - Kx^2 - Ky^2) of the elements this thread holds: z-independent, computed once
+    // per column (the per-z work is then one product and one sincos per element)
+    float sq[MBL][RL];
+#pragma unroll
+    for (int m = 0; m < MBL; ++m)
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        const float Kx = kfreq(freq_index(tid + m * TT + r * (PN / RL), PN), PN, a.dx);
+        sq[m][r] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
+      }
     __syncthreads();  // mz visible
     for (int zz = z_lo; zz < z_hi; ++zz) {
       const float z = a.zv[a.zoff + zz];
@@ -296,17 +314,14 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
       auto ld1 = [&](int m, int r, int idx) {
         const int mx = freq_index(idx, PN);
         if (mx > M || -mx > M) return make_float2(0.f, 0.f);
-        // sqrt(k^2 - Kx^2 - Ky^2) recomputed per z (register pressure of the radix-16 head)
-        const float Kx = kfreq(mx, PN, a.dx);
-        const float sq = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
         float sn, cs;
-        sincos_hw(tf_mul(z, sq), &sn, &cs);
+        sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
         return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
       };
       float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+        if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v;
       };
       fft_pow2_io<true, PN, TT, false, false, false>(lds, twl, tz, ld1, sv1);
     }

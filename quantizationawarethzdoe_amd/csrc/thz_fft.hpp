@@ -414,7 +414,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
       const int i = tid + m * T;
-      const int k = i & (L - 1);
+      const int k = L * R == N ? i : i & (L - 1);  // last stage: i < N / R = L
       const int j = (i - k) * R + k;
 #pragma unroll
       for (int r = 0; r < R; ++r) sv(m, r, j + r * L, v[m][r]);
