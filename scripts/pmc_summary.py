@@ -39,7 +39,7 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     summ = {}
-    for sub in ("fetch", "write", "sq"):
+    for sub in ("fetch", "write", "sq", "sq2"):
         p = os.path.join(src, sub, "run_counter_collection.csv")
         if os.path.exists(p):
             for k, d in per_kernel(p).items():
