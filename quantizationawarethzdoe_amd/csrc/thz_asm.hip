@@ -153,7 +153,7 @@ __device__ __forceinline__ float2 vrs_ez(float2 ex, float2 ey, float x, float y,
 #pragma clang fp contract(on)
 
 template <int PN>
-__global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
+__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
                                                     FftPlan pw, AsmArgs a) {
   extern __shared__ float2 lds[];
   const int row = xcd_rows(blockIdx.x, gridDim.x);
@@ -172,7 +172,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
     return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
   };
   if constexpr (PN > 0) {
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     auto ld = [&](int, int, int idx) {
       const int s = idx - a.in_c0;
       return (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(1024) asm_rows_fwd(const float2* __restrict__ 
       const int c = band_col(j, PN, a.J, a.ncols);
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
-    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
@@ -364,7 +364,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
 // K3: per output row: gather band from U, IFFT(Pw), crop -> out[z][bc][r][w]
 // ---------------------------------------------------------------------------------------------
 template <int PN>
-__global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ U, float2* __restrict__ out,
+__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* __restrict__ U, float2* __restrict__ out,
                                                     FftPlan pw, AsmArgs a) {
   extern __shared__ float2 lds[];
   const int row = xcd_rows(blockIdx.x, gridDim.x);  // row in [0, nz*BC*Hout)
@@ -373,7 +373,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
   const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
   if constexpr (PN > 0) {
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     // First stage (radix 16, L = 1) reads j = i + q*NB0, i < NB0.  Its band column is
     // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
     // frequencies), a multiple of CBU: the blocked address is then base(c0) + delta_q*Hout,
@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(1024) asm_rows_inv(const float2* __restrict__ 
       const int w = j - a.out_c0;
       if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
     };
-    fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<true, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);
@@ -431,10 +431,10 @@ __global__ void __launch_bounds__(1024) rsc_k_rows(float2* __restrict__ TK, FftP
   auto store = [&](int j, float2 v) { dst[blk(band_col(j, k.Pw, k.Pw / 2, k.Pw), i, k.Ph)] = v; };
   const int tid = threadIdx.x, nt = blockDim.x;
   if constexpr (PN > 0) {
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pw.tw, tid, nt);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     auto ld = [&](int, int, int j) { return load(j); };
     auto sv = [&](int, int, int j, float2 v) { store(j, v); };
-    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < k.Pw; j += nt) lds[padx(j)] = load(j);
     __syncthreads();
@@ -453,10 +453,10 @@ __global__ void __launch_bounds__(1024) rsc_k_cols(const float2* __restrict__ TK
   float2* dst = KF + ((size_t)c * k.Pw + cc) * k.Ph;
   const int tid = threadIdx.x, nt = blockDim.x;
   if constexpr (PN > 0) {
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), ph.tw, tid, nt);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), ph.tw, tid, nt);
     auto ld = [&](int, int, int i) { return col[(size_t)i * CB]; };
     auto sv = [&](int, int, int i, float2 v) { dst[i] = v; };
-    fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
   } else {
     for (int i = tid; i < k.Ph; i += nt) lds[padx(i)] = col[(size_t)i * CB];
     __syncthreads();
@@ -475,11 +475,11 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
   const int tid = threadIdx.x, nt = blockDim.x;
   const size_t base = (size_t)blockIdx.x * p.n;
   if constexpr (PN > 0) {
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), p.tw, tid, nt);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), p.tw, tid, nt);
     auto ld = [&](int, int, int j) { return in[base + j]; };
     auto sv = [&](int, int, int j, float2 v) { out[base + j] = v; };
-    if (inverse) fft_pow2_io<true, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
-    else fft_pow2_io<false, PN, Geo<PN>::T, false, false, false>(lds, twl, tid, ld, sv);
+    if (inverse) fft_pow2_run<true, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
+    else fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];
     __syncthreads();
@@ -686,7 +686,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
   const int tw = threads_for(g.Pw), th = threads_for(g.Ph);
   {
     KernelTimer kt("asm_rows_fwd", s);
-    THZ_POW2_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), dim3(tw), fft_lds_bytes(g.Pw), s, (const float2*)in,
+    THZ_POW2_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), dim3(tw), fft_lds_bytes_io(g.Pw), s, (const float2*)in,
                     T, pw, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
@@ -704,7 +704,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     }
     {
       KernelTimer kt("asm_rows_inv", s);
-      THZ_POW2_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), dim3(tw), fft_lds_bytes(g.Pw), s,
+      THZ_POW2_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), dim3(tw), fft_lds_bytes_io(g.Pw), s,
                       (const float2*)U, (float2*)out, pw, a);
       THZ_LAUNCH_CHECK();
       kt.stop();
@@ -788,7 +788,7 @@ extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inve
   int e = get_plan(n, &p);
   if (e) return e;
   if ((e = ensure_lds_attr())) return e;
-  THZ_POW2_SWITCH(n, fft_rows_kernel, dim3(rows), dim3(threads_for(n)), fft_lds_bytes(n), (hipStream_t)stream,
+  THZ_POW2_SWITCH(n, fft_rows_kernel, dim3(rows), dim3(threads_for(n)), fft_lds_bytes_io(n), (hipStream_t)stream,
                   (const float2*)in, (float2*)out, p, inverse);
   THZ_LAUNCH_CHECK();
   return THZ_OK;
@@ -873,10 +873,10 @@ extern "C" int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out,
   float2* U = (float2*)(w + p.tk + p.kf + p.t);
   {
     KernelTimer kt("rsc_kernel_fft", s);
-    THZ_POW2_SWITCH(g.Pw, rsc_k_rows, dim3(d->C * g.Ph), dim3(threads_for(g.Pw)), fft_lds_bytes(g.Pw), s, TK, pw,
+    THZ_POW2_SWITCH(g.Pw, rsc_k_rows, dim3(d->C * g.Ph), dim3(threads_for(g.Pw)), fft_lds_bytes_io(g.Pw), s, TK, pw,
                     p.k);
     THZ_LAUNCH_CHECK();
-    THZ_POW2_SWITCH(g.Ph, rsc_k_cols, dim3(d->C * g.Pw), dim3(threads_for(g.Ph)), fft_lds_bytes(g.Ph), s,
+    THZ_POW2_SWITCH(g.Ph, rsc_k_cols, dim3(d->C * g.Pw), dim3(threads_for(g.Ph)), fft_lds_bytes_io(g.Ph), s,
                     (const float2*)TK, KF, ph, p.k);
     THZ_LAUNCH_CHECK();
     kt.stop();

@@ -139,14 +139,14 @@ __global__ void __launch_bounds__(1024) czt_rows(const float2* __restrict__ in, 
     constexpr int RL = S::radix(S::NST - 1, false);
     constexpr int MBL = PN / RL / TT;
     float2 sp[MBL][RL];
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pl.tw, tid, blockDim.x);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pl.tw, tid, blockDim.x);
     auto ld0 = [&](int, int, int idx) { return load_x(idx); };
     auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
+    fft_pow2_run<false, PN, TT, false>(lds, twl, tid, ld0, sv0);
     asm volatile("" : "+v"(tid));
     auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
     auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tid, ld1, sv1);
+    fft_pow2_run<true, PN, TT, true>(lds, twl, tid, ld1, sv1);
   } else {
     const int n = pl.n, nt = blockDim.x;
     for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
@@ -197,14 +197,14 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
     constexpr int RL = S::radix(S::NST - 1, false);
     constexpr int MBL = PN / RL / TT;
     float2 sp[MBL][RL];
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pl.tw, tid, blockDim.x);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pl.tw, tid, blockDim.x);
     auto ld0 = [&](int, int, int idx) { return load_x(idx); };
     auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
+    fft_pow2_run<false, PN, TT, false>(lds, twl, tid, ld0, sv0);
     asm volatile("" : "+v"(tid));
     auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
     auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tid, ld1, sv1);
+    fft_pow2_run<true, PN, TT, true>(lds, twl, tid, ld1, sv1);
   } else {
     const int n = pl.n, nt = blockDim.x;
     for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
@@ -237,14 +237,14 @@ __device__ __forceinline__ void czt_adj_line(float2* lds, const FftPlan& pl, con
     constexpr int RL = S::radix(S::NST - 1, false);
     constexpr int MBL = PN / RL / TT;
     float2 sp[MBL][RL];
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), pl.tw, tid, blockDim.x);
+    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pl.tw, tid, blockDim.x);
     auto ld0 = [&](int, int, int idx) { return load_x(idx); };
     auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    fft_pow2_io<false, PN, TT, false, false, false>(lds, twl, tid, ld0, sv0);
+    fft_pow2_run<false, PN, TT, false>(lds, twl, tid, ld0, sv0);
     asm volatile("" : "+v"(tid));
     auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], conjf2(ft[idx])); };
     auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    fft_pow2_io<true, PN, TT, true, false, false>(lds, twl, tid, ld1, sv1);
+    fft_pow2_run<true, PN, TT, true>(lds, twl, tid, ld1, sv1);
   } else {
     const int n = pl.n, nt = blockDim.x;
     for (int j = tid; j < n; j += nt) lds[padx(j)] = load_x(j);
@@ -492,10 +492,10 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   if (d->adjoint) {  // G [B, C, outW, outH] -> grad_in [B, C, H, W]: column pass first
     KernelTimer kt("czt_adjoint", s);
     THZ_CZT_SWITCH(a.pb.np2, czt_cols_adj, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
-                   fft_lds_bytes(a.pb.np2), s, (const float2*)in, V, (const float2*)ws, plB, a);
+                   fft_lds_bytes_io(a.pb.np2), s, (const float2*)in, V, (const float2*)ws, plB, a);
     THZ_LAUNCH_CHECK();
     THZ_CZT_SWITCH(a.pa.np2, czt_rows_adj, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
-                   fft_lds_bytes(a.pa.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plA, a);
+                   fft_lds_bytes_io(a.pa.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plA, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
     return THZ_OK;
@@ -503,14 +503,14 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   {
     KernelTimer kt("czt_rows", s);
     THZ_CZT_SWITCH(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
-                   fft_lds_bytes(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
+                   fft_lds_bytes_io(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
   {
     KernelTimer kt("czt_cols", s);
     THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
-                   fft_lds_bytes(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
+                   fft_lds_bytes_io(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
   }

@@ -23,6 +23,13 @@
 namespace thz {
 
 constexpr int FFT_MAX_STAGES = 24;
+#ifndef THZ_SPLIT
+#define THZ_SPLIT 1
+#endif
+// Split-exchange row kernels of 8192 / 16384 points: the LDS image allows 8 waves / SIMD, so
+// hold them to 64 VGPRs (the smaller sizes are LDS-limited below 8 and would only spill).
+__host__ __device__ constexpr int row_waves_per_eu(int n) { return THZ_SPLIT && n >= 8192 ? 8 : 1; }
+#define THZ_ROW_ATTR __attribute__((amdgpu_waves_per_eu(row_waves_per_eu(PN))))
 constexpr int FFT_MAXV = 16;  // complex values held per thread per stage (N <= 16 * threads)
 #ifndef THZ_PV
 #define THZ_PV 16
@@ -462,6 +469,109 @@ __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, 
     stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS>(lds, tw, tid, ld, sv);
     fft_pow2_io<INV, N, T, SMALL_FIRST, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split-exchange form of the power-of-two transform.  The LDS image holds ONE float per
+// element; each Stockham exchange moves the real parts, then the imaginary parts (four
+// barriers instead of two).  The data image is half the size (N floats + padding), so twice as
+// many workgroups fit on a CU -- for a latency-bound row pass that is the larger effect.
+// Stage 0 reads through ld(m, r, idx), the last stage writes through sv(m, r, idx, v); every
+// stage keeps its butterflies' operands in registers (the exchange lands them there directly).
+__host__ __device__ constexpr int lds_split_f2(int n) { return (lds_floats2(n) + 1) / 2; }
+
+template <int R, bool INV, int N, int L, int T, class Tw, class In>
+__device__ __forceinline__ void stage_core(const Tw& tw, int tid, In& in, float2 (&v)[N / R / T][R]) {
+  constexpr int NB = N / R;
+  constexpr int MB = NB / T;
+  static_assert(MB * T == NB, "pow2 plan must tile exactly");
+  constexpr int TWS = N / (L * R);
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int i = tid + m * T;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[m][r] = in(m, r, i + r * NB);
+    if constexpr (L > 1) {
+      float2 w[R];
+      if constexpr (L * R == 256 && std::is_same<Tw, TwLds>::value) {
+        const int k = i & (L - 1);
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          w[r] = tw.t256[k * r];
+          if (INV) w[r].y = -w[r].y;
+        }
+      } else {
+        twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
+      }
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[m][r] = cmul(v[m][r], w[r]);
+    }
+    dftR<R, INV>(v[m]);
+  }
+}
+
+template <bool INV, int N, int T, bool SMALL_FIRST, int S = 0, int L = 1, class Tw, class In, class Sv>
+__device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int tid, In& in, Sv& sv) {
+  using P = Pow2Sched<N>;
+  constexpr int R = P::radix(S, SMALL_FIRST);
+  constexpr int MB = N / R / T;
+  float2 v[MB][R];
+  stage_core<R, INV, N, L, T>(tw, tid, in, v);
+  if constexpr (S == P::NST - 1) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int i = tid + m * T;
+#pragma unroll
+      for (int r = 0; r < R; ++r) sv(m, r, i + r * L, v[m][r]);  // last stage: L R = N, k = i
+    }
+  } else {
+    constexpr int R2 = P::radix(S + 1, SMALL_FIRST);
+    constexpr int NB2 = N / R2;
+    constexpr int MB2 = NB2 / T;
+    static_assert(NB2 % 16 == 0, "constant-offset LDS addressing");
+    float2 nx[MB2][R2];
+    // output element j = (i - k) R + k + r L of this stage -> input i2 + r2 NB2 of the next
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      __syncthreads();  // previous readers of the image are done
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+        const int i = tid + m * T;
+        const int k = i & (L - 1);
+        float* dst = lds + padx((i - k) * R + k);
+#pragma unroll
+        for (int r = 0; r < R; ++r) dst[r * L + ((r * L) >> 4)] = part ? v[m][r].y : v[m][r].x;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < MB2; ++m) {
+        const float* src = lds + padx(tid + m * T);
+#pragma unroll
+        for (int r = 0; r < R2; ++r) {
+          const float x = src[r * NB2 + ((r * NB2) >> 4)];
+          if (part) nx[m][r].y = x;
+          else nx[m][r].x = x;
+        }
+      }
+    }
+    auto in2 = [&](int m, int r, int) { return nx[m][r]; };
+    fft_pow2_split_io<INV, N, T, SMALL_FIRST, S + 1, L * R>(lds, tw, tid, in2, sv);
+  }
+}
+
+// The row / column kernels' transform: split exchanges (THZ_SPLIT, the default) or the complex
+// image; tw_slot is where that kernel's twiddle tables start in LDS.
+template <int N>
+__device__ __forceinline__ float2* tw_slot(float2* lds) {
+  return lds + (THZ_SPLIT ? lds_split_f2(N) : lds_floats2(N));
+}
+template <bool INV, int N, int T, bool SMALL_FIRST, class Tw, class Ld, class Sv>
+__device__ __forceinline__ void fft_pow2_run(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
+#if THZ_SPLIT
+  fft_pow2_split_io<INV, N, T, SMALL_FIRST>(reinterpret_cast<float*>(lds), tw, tid, ld, sv);
+#else
+  fft_pow2_io<INV, N, T, SMALL_FIRST, false, false>(lds, tw, tid, ld, sv);
+#endif
 }
 
 // Whole transform with the data in LDS (natural order in and out).
