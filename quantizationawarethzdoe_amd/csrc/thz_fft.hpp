@@ -49,17 +49,78 @@ struct FftPlan {
 __device__ __forceinline__ int padx(int a) { return a + (a >> 4); }
 __host__ __device__ constexpr int lds_floats2(int n) { return n + (n >> 4) + 1; }
 
+// Complex arithmetic.  THZ_PK=1 builds it on packed fp32: a complex value is one 64-bit VGPR
+// pair and every operation is one v_pk_{add,mul,fma}_f32, with the swaps and sign flips of a
+// complex product / a multiply by -+i on the op_sel / neg modifiers (inline asm: the compiler
+// would materialise them as moves).  That halves the VALU instruction count of a butterfly but
+// not its issue cycles (a packed op occupies the SIMD-32 for both halves), and the aligned
+// register pairs push the column pass into spills: measured on cfg2, K3 -1 %, K2 +10 %.  The
+// scalar form is the default.
+#ifndef THZ_PK
+#define THZ_PK 0
+#endif
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk(float2 a) { return (pf2){a.x, a.y}; }
+__device__ __forceinline__ float2 upk(pf2 a) { return make_float2(a.x, a.y); }
+
+#if THZ_PK
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return upk(pk(a) + pk(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return upk(pk(a) - pk(b)); }
+// (a.x b.x - a.y b.y, a.x b.y + a.y b.x): t = a.xx * b, then fma((a.y, a.y), (b.y, b.x), t) with
+// the low product negated
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  const pf2 pa = pk(a), pb = pk(b);
+  const pf2 t = pa.xx * pb;
+  pf2 r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(pa), "v"(pb), "v"(t));
+  return upk(r);
+}
+// a * conj(b) = (a.x b.x + a.y b.y, a.y b.x - a.x b.y)
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+  pf2 t, r;
+  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(b)), "v"(t));
+  return upk(r);
+}
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return upk(pk(a) * s); }
+// a + (-i) d = (a.x + d.y, a.y - d.x)   and   a - (-i) d = (a.x - d.y, a.y + d.x)
+__device__ __forceinline__ float2 add_mfwd(float2 a, float2 d) {
+  pf2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
+  return upk(r);
+}
+__device__ __forceinline__ float2 sub_mfwd(float2 a, float2 d) {
+  pf2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
+  return upk(r);
+}
+#else
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
+__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
+  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+}
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+__device__ __forceinline__ float2 add_mfwd(float2 a, float2 d) { return make_float2(a.x + d.y, a.y - d.x); }
+__device__ __forceinline__ float2 sub_mfwd(float2 a, float2 d) { return make_float2(a.x - d.y, a.y + d.x); }
+#endif
+// a * w (forward) or a * conj(w) (inverse): twiddles are stored and combined unconjugated
+template <bool INV>
+__device__ __forceinline__ float2 cmul_tw(float2 a, float2 w) { return INV ? cmulc(a, w) : cmul(a, w); }
 // multiply by -i (forward) or +i (inverse)
 template <bool INV>
 __device__ __forceinline__ float2 mul_mi(float2 a) {
   return INV ? make_float2(-a.y, a.x) : make_float2(a.y, -a.x);
 }
+// a + m d and a - m d with m = -i (forward) or +i (inverse): one packed add each
+template <bool INV>
+__device__ __forceinline__ float2 add_mi(float2 a, float2 d) { return INV ? sub_mfwd(a, d) : add_mfwd(a, d); }
+template <bool INV>
+__device__ __forceinline__ float2 sub_mi(float2 a, float2 d) { return INV ? add_mfwd(a, d) : sub_mfwd(a, d); }
 
 // ---------------------------------------------------------------------------------------------
 // In-register DFTs: y_q = sum_r v_r exp(-+2 pi i r q / R)
@@ -74,11 +135,22 @@ __device__ __forceinline__ void dft2(float2& a, float2& b) {
 template <bool INV>
 __device__ __forceinline__ void dft4(float2& a0, float2& a1, float2& a2, float2& a3) {
   float2 t0 = cadd(a0, a2), t1 = csub(a0, a2);
-  float2 t2 = cadd(a1, a3), t3 = mul_mi<INV>(csub(a1, a3));
+  float2 t2 = cadd(a1, a3), d = csub(a1, a3);
   a0 = cadd(t0, t2);
   a2 = csub(t0, t2);
-  a1 = cadd(t1, t3);
-  a3 = csub(t1, t3);
+  a1 = add_mi<INV>(t1, d);
+  a3 = sub_mi<INV>(t1, d);
+}
+// dft4 of (a0, a1, m a2, a3) with m = -i (forward) / +i (inverse): the twiddle of the radix-16
+// element (2, 2) folded into the first butterfly
+template <bool INV>
+__device__ __forceinline__ void dft4_m2(float2& a0, float2& a1, float2& a2, float2& a3) {
+  float2 t0 = add_mi<INV>(a0, a2), t1 = sub_mi<INV>(a0, a2);
+  float2 t2 = cadd(a1, a3), d = csub(a1, a3);
+  a0 = cadd(t0, t2);
+  a2 = csub(t0, t2);
+  a1 = add_mi<INV>(t1, d);
+  a3 = sub_mi<INV>(t1, d);
 }
 
 template <bool INV>
@@ -89,23 +161,15 @@ __device__ __forceinline__ void dft8(float2* v) {
   dft4<INV>(e0, e1, e2, e3);
   dft4<INV>(o0, o1, o2, o3);
   const float c = 0.70710678118654752440f;
-  // w8^1 * o1, w8^2 * o2, w8^3 * o3 ; w8 = exp(-+i pi/4)
-  float2 t1, t2, t3;
-  if (!INV) {
-    t1 = make_float2(c * (o1.x + o1.y), c * (o1.y - o1.x));
-    t2 = make_float2(o2.y, -o2.x);
-    t3 = make_float2(c * (o3.y - o3.x), -c * (o3.x + o3.y));
-  } else {
-    t1 = make_float2(c * (o1.x - o1.y), c * (o1.y + o1.x));
-    t2 = make_float2(-o2.y, o2.x);
-    t3 = make_float2(-c * (o3.x + o3.y), c * (o3.x - o3.y));
-  }
+  // w8^1 o1 = c (o1 + m o1), w8^3 o3 = -c (o3 - m o3), w8^2 o2 = m o2 (m = -+i)
+  const float2 t1 = cscale(add_mi<INV>(o1, o1), c);
+  const float2 t3 = cscale(sub_mi<INV>(o3, o3), -c);
   v[0] = cadd(e0, o0);
   v[4] = csub(e0, o0);
   v[1] = cadd(e1, t1);
   v[5] = csub(e1, t1);
-  v[2] = cadd(e2, t2);
-  v[6] = csub(e2, t2);
+  v[2] = add_mi<INV>(e2, o2);
+  v[6] = sub_mi<INV>(e2, o2);
   v[3] = cadd(e3, t3);
   v[7] = csub(e3, t3);
 }
@@ -126,19 +190,20 @@ __device__ __forceinline__ void dft16(float2* v) {
   // w16^k = cos(2 pi k/16) + s i sin(2 pi k/16), k = r2*q1 in {1,2,3,4,6,9}
   const float c1 = 0.92387953251128675613f, s1 = 0.38268343236508977173f;
   const float c2 = 0.70710678118654752440f;
+  // w16^2 = c2 (1 + m), w16^6 = -c2 (1 - m) with m = -+i; w16^4 = m (folded into dft4_m2)
   b[1][1] = cmul(b[1][1], make_float2(c1, s * s1));
-  b[1][2] = cmul(b[1][2], make_float2(c2, s * c2));
+  b[1][2] = cscale(add_mi<INV>(b[1][2], b[1][2]), c2);
   b[1][3] = cmul(b[1][3], make_float2(s1, s * c1));
-  b[2][1] = cmul(b[2][1], make_float2(c2, s * c2));
-  b[2][2] = mul_mi<INV>(b[2][2]);
-  b[2][3] = cmul(b[2][3], make_float2(-c2, s * c2));
+  b[2][1] = cscale(add_mi<INV>(b[2][1], b[2][1]), c2);
+  b[2][3] = cscale(sub_mi<INV>(b[2][3], b[2][3]), -c2);
   b[3][1] = cmul(b[3][1], make_float2(s1, s * c1));
-  b[3][2] = cmul(b[3][2], make_float2(-c2, s * c2));
+  b[3][2] = cscale(sub_mi<INV>(b[3][2], b[3][2]), -c2);
   b[3][3] = cmul(b[3][3], make_float2(-c1, -s * s1));
 #pragma unroll
   for (int q1 = 0; q1 < 4; ++q1) {
     float2 a0 = b[0][q1], a1 = b[1][q1], a2 = b[2][q1], a3 = b[3][q1];
-    dft4<INV>(a0, a1, a2, a3);
+    if (q1 == 2) dft4_m2<INV>(a0, a1, a2, a3);
+    else dft4<INV>(a0, a1, a2, a3);
     v[q1] = a0;
     v[q1 + 4] = a1;
     v[q1 + 8] = a2;
@@ -233,12 +298,11 @@ __device__ __noinline__ void stage_reg(float2* lds, int n, int L, const float2* 
       for (int r = 0; r < R; ++r) v[m][r] = lds[padx(i + r * nb)];
       if (L > 1) {
         const int k = i % L;
-        float2 w = tw[k * twstep];
-        if (INV) w.y = -w.y;
+        const float2 w = tw[k * twstep];
         float2 wr = w;
 #pragma unroll
         for (int r = 1; r < R; ++r) {
-          v[m][r] = cmul(v[m][r], wr);
+          v[m][r] = cmul_tw<INV>(v[m][r], wr);
           if (r + 1 < R) wr = cmul(wr, w);
         }
       }
@@ -340,17 +404,14 @@ __device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restri
   return TwLds{dst, dst + N2};
 }
 
-template <int R, bool INV, class Tw>
+template <int R, class Tw>
 __device__ __forceinline__ void twiddle_powers(const Tw& tw, int kt, float2* w) {
-  // w[r] for r = 1..R-1 ; kt = k * (N / (L R)) is the table index of w^1
+  // w[r] for r = 1..R-1 (forward sign; the inverse applies them conjugated, cmul_tw);
+  // kt = k * (N / (L R)) is the table index of w^1
   w[1] = twat(tw, kt);
   if constexpr (R >= 4) w[2] = twat(tw, 2 * kt);
   if constexpr (R >= 8) w[4] = twat(tw, 4 * kt);
   if constexpr (R >= 16) w[8] = twat(tw, 8 * kt);
-  if (INV) {
-#pragma unroll
-    for (int p = 1; p < R; p <<= 1) w[p].y = -w[p].y;
-  }
   if constexpr (R >= 4) w[3] = cmul(w[1], w[2]);
   if constexpr (R >= 8) {
     w[5] = cmul(w[1], w[4]);
@@ -369,7 +430,19 @@ __device__ __forceinline__ void twiddle_powers(const Tw& tw, int kt, float2* w) 
 // For power-of-two N >= 256 every LDS access is base + compile-time offset:
 //   padx(i + r NB) = padx(i) + r NB + (r NB >> 4)       (NB % 16 == 0)
 //   padx(j + r L)  = padx(j) + r L  + (r L >> 4)        (L | 16 or 16 | L, L R >= 16 or L == 1)
-template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, class Tw, class Ld, class Sv>
+// Complex-image layouts per exchange (keyed by the writing stage's L): element j at float2
+// j + C (j >> SH).  L == 1 keeps padx (the natural-order image fft_pow2's callers read and
+// write); 1 < L < 16 uses (4 + log2 L, L); L >= 16 needs no padding.  Bank model of ds_read_b64
+// (2 x 32 lanes, dword mod 64) and ds_write_b64 (4 x 16 lanes, dword mod 32): 1.33x the ideal
+// LDS cycles on the L == 1 exchange, conflict-free on the others (scripts/lds_bank_sim.py
+// layouts64), against 1.33x on every exchange for padx everywhere.
+__host__ __device__ constexpr int c64_sh(int L) { return L == 1 ? 4 : (L < 16 ? 4 + pow2_log(L) : 0); }
+__host__ __device__ constexpr int c64_c(int L) { return L == 1 ? 1 : (L < 16 ? L : 0); }
+template <int L>
+__host__ __device__ constexpr int c64_lay(int j) { return j + c64_c(L) * (j >> c64_sh(L)); }
+
+template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, int LIN = 1, int LOUT = L, class Tw,
+          class Ld, class Sv>
 __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
   constexpr int NB = N / R;
   constexpr int MB = NB / T;  // butterflies per thread (exact)
@@ -381,9 +454,9 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
   for (int m = 0; m < MB; ++m) {
     const int i = tid + m * T;
     if constexpr (IN_LDS) {
-      const float2* src = lds + padx(i);
+      const float2* src = lds + c64_lay<LIN>(i);
 #pragma unroll
-      for (int r = 0; r < R; ++r) v[m][r] = src[r * NB + ((r * NB) >> 4)];
+      for (int r = 0; r < R; ++r) v[m][r] = src[c64_lay<LIN>(m * T + r * NB) - c64_lay<LIN>(m * T)];
     } else {
 #pragma unroll
       for (int r = 0; r < R; ++r) v[m][r] = ld(m, r, i + r * NB);
@@ -391,18 +464,15 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     if constexpr (L > 1) {
       float2 w[R];
       if constexpr (L * R == 256 && std::is_same<Tw, TwLds>::value) {
-        // w^r = exp(-+2 pi i k r / 256) with k r <= 225: straight LDS reads, no products
+        // w^r = exp(-2 pi i k r / 256) with k r <= 225: straight LDS reads, no products
         const int k = i & (L - 1);
 #pragma unroll
-        for (int r = 1; r < R; ++r) {
-          w[r] = tw.t256[k * r];
-          if (INV) w[r].y = -w[r].y;
-        }
+        for (int r = 1; r < R; ++r) w[r] = tw.t256[k * r];
       } else {
-        twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
+        twiddle_powers<R>(tw, (i & (L - 1)) * TWS, w);
       }
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[m][r] = cmul(v[m][r], w[r]);
+      for (int r = 1; r < R; ++r) v[m][r] = cmul_tw<INV>(v[m][r], w[r]);
     }
     dftR<R, INV>(v[m]);
   }
@@ -412,9 +482,10 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     for (int m = 0; m < MB; ++m) {
       const int i = tid + m * T;
       const int k = i & (L - 1);
-      float2* dst = lds + padx((i - k) * R + k);
+      const int i0 = m * T, k0 = i0 & (L - 1), j0 = (i0 - k0) * R + k0;  // thread 0: folds after unrolling
+      float2* dst = lds + c64_lay<LOUT>((i - k) * R + k);
 #pragma unroll
-      for (int r = 0; r < R; ++r) dst[r * L + ((r * L) >> 4)] = v[m][r];
+      for (int r = 0; r < R; ++r) dst[c64_lay<LOUT>(j0 + r * L) - c64_lay<LOUT>(j0)] = v[m][r];
     }
     __syncthreads();
   } else {
@@ -466,7 +537,10 @@ __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, 
     constexpr int R = P::radix(S, SMALL_FIRST);
     constexpr bool IN_LDS = S > 0 || FIRST_LDS;
     constexpr bool OUT_LDS = S < P::NST - 1 || LAST_LDS;
-    stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS>(lds, tw, tid, ld, sv);
+    // image layouts: the previous stage's (L / its radix); natural-order padx at the two ends
+    constexpr int LIN = S == 0 ? 1 : L / P::radix(S - 1, SMALL_FIRST);
+    constexpr int LOUT = S == P::NST - 1 ? 1 : L;
+    stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv);
     fft_pow2_io<INV, N, T, SMALL_FIRST, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
   }
 }
@@ -496,19 +570,28 @@ __device__ __forceinline__ void stage_core(const Tw& tw, int tid, In& in, float2
       if constexpr (L * R == 256 && std::is_same<Tw, TwLds>::value) {
         const int k = i & (L - 1);
 #pragma unroll
-        for (int r = 1; r < R; ++r) {
-          w[r] = tw.t256[k * r];
-          if (INV) w[r].y = -w[r].y;
-        }
+        for (int r = 1; r < R; ++r) w[r] = tw.t256[k * r];
       } else {
-        twiddle_powers<R, INV>(tw, (i & (L - 1)) * TWS, w);
+        twiddle_powers<R>(tw, (i & (L - 1)) * TWS, w);
       }
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[m][r] = cmul(v[m][r], w[r]);
+      for (int r = 1; r < R; ++r) v[m][r] = cmul_tw<INV>(v[m][r], w[r]);
     }
     dftR<R, INV>(v[m]);
   }
 }
+
+// LDS layout of one split exchange: element j lives at float j + C (j >> SH).  Chosen per
+// exchange (by the writing stage's L) so that its write pattern (j = (i - k) R + k + r L) and the
+// next stage's read pattern (i + r N/R2) are both free of bank conflicts under the ds_read_b32 /
+// ds_write_b32 banking (two 32-lane groups, bank = dword mod 32; MI355X_MICROARCH.md §LDS), and
+// the r-offsets stay compile-time constants.  Found by search (scripts/lds_bank_sim.py layouts)
+// for every power-of-two size and both schedules; all fit in N + N/16 floats.  The fixed
+// j + (j >> 4) it replaces costs 67 % extra LDS cycles on the 8192-point schedule.
+__host__ __device__ constexpr int split_sh(int L) { return L == 1 ? 5 : (L <= 16 ? 4 + pow2_log(L) : 11); }
+__host__ __device__ constexpr int split_c(int L) { return L == 1 ? 1 : (L <= 16 ? L : 1); }
+template <int L>
+__host__ __device__ constexpr int split_lay(int j) { return j + split_c(L) * (j >> split_sh(L)); }
 
 template <bool INV, int N, int T, bool SMALL_FIRST, int S = 0, int L = 1, class Tw, class In, class Sv>
 __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int tid, In& in, Sv& sv) {
@@ -528,9 +611,10 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
     constexpr int R2 = P::radix(S + 1, SMALL_FIRST);
     constexpr int NB2 = N / R2;
     constexpr int MB2 = NB2 / T;
-    static_assert(NB2 % 16 == 0, "constant-offset LDS addressing");
+    static_assert(split_lay<L>(N - 1) < 2 * lds_split_f2(N), "split layout exceeds the LDS image");
     float2 nx[MB2][R2];
-    // output element j = (i - k) R + k + r L of this stage -> input i2 + r2 NB2 of the next
+    // output element j = (i - k) R + k + r L of this stage -> input i2 + r2 NB2 of the next; the
+    // per-r address offsets are those of thread 0 (constant over threads for these layouts)
 #pragma unroll
     for (int part = 0; part < 2; ++part) {
       __syncthreads();  // previous readers of the image are done
@@ -538,17 +622,19 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
       for (int m = 0; m < MB; ++m) {
         const int i = tid + m * T;
         const int k = i & (L - 1);
-        float* dst = lds + padx((i - k) * R + k);
+        const int i0 = m * T, k0 = i0 & (L - 1), j0 = (i0 - k0) * R + k0;  // folds after unrolling
+        float* dst = lds + split_lay<L>((i - k) * R + k);
 #pragma unroll
-        for (int r = 0; r < R; ++r) dst[r * L + ((r * L) >> 4)] = part ? v[m][r].y : v[m][r].x;
+        for (int r = 0; r < R; ++r)
+          dst[split_lay<L>(j0 + r * L) - split_lay<L>(j0)] = part ? v[m][r].y : v[m][r].x;
       }
       __syncthreads();
 #pragma unroll
       for (int m = 0; m < MB2; ++m) {
-        const float* src = lds + padx(tid + m * T);
+        const float* src = lds + split_lay<L>(tid + m * T);
 #pragma unroll
         for (int r = 0; r < R2; ++r) {
-          const float x = src[r * NB2 + ((r * NB2) >> 4)];
+          const float x = src[split_lay<L>(m * T + r * NB2) - split_lay<L>(m * T)];
           if (part) nx[m][r].y = x;
           else nx[m][r].x = x;
         }
