@@ -145,6 +145,45 @@ def bench_qat(dev, rank, world, steps=60, dist=None):
                         "HIP-graph replay per schedule phase, gradient all-reduce over ranks", "phases": out}
 
 
+def bench_donn(dev, rank, world, steps=20, warmup=3, dist=None):
+    """cfg5 (secondary line): 3-layer DONN (100^2 fields, ASM P = 300 between layers, the
+    FullPrecision DOE layers the notebook instantiates) training step on a global batch of 256
+    split over the ranks: forward, detector-target loss, backward, one-bucket gradient all-reduce
+    (3 x 100^2 fp32 = 120 KB), Adam; HIP-graph replay.  Synthetic digits: uniform [0, 1) images
+    and random labels (seed = rank); identical initial weights on every rank."""
+    from quantizationawarethzdoe_amd import donn
+    per = len(shard_planes(256, rank, world))
+    g = torch.Generator().manual_seed(rank)
+    u = torch.rand(per, 1, 100, 100, generator=g).to(dev)
+    labels = torch.randint(0, 10, (per,), generator=g).to(dev)
+    targets = donn.detector_targets(device=dev)
+    out = {}
+    for name, chained in (("chained", True), ("notebook", False)):
+        torch.manual_seed(1234)  # same initial weights on every rank
+        model = donn.DONN(device=dev)
+        torch.manual_seed(1234 + rank)  # per-rank height-noise draws
+        tr = donn.DONNTrainer(model, targets, graph=True, chained=chained)
+        for _ in range(warmup):
+            tr.step(u, labels)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = tr.step(u, labels)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out[name] = {"samples_per_s": round(256 * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+                     "loss": round(float(loss.detach()), 6)}
+    return {"workload": "cfg5: 3-layer DONN (100^2, P=300 ASM, FullPrecision DOE layers) training step, global "
+                        "batch 256 split over ranks, detector-target loss, gradient all-reduce, Adam, HIP-graph "
+                        "replay; synthetic digits", "per_rank_batch": per, "modes": out}
+
+
 def load_traffic():
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -164,7 +203,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--z-chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 secondary measurements")
+    ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 / cfg5 secondary measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -278,7 +317,7 @@ def main():
     if not args.headline_only:
         # secondary workloads never take the headline line down with them
         line["secondary"] = {}
-        for key, fn in (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat)):
+        for key, fn in (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat), ("cfg5_donn", bench_donn)):
             try:
                 line["secondary"][key] = fn(dev, rank, world, dist=dist)
             except Exception as e:  # noqa: BLE001 -- reported in the JSON line

@@ -21,6 +21,7 @@ import os
 
 import numpy as np
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
@@ -77,12 +78,16 @@ class DONN(nn.Module):
                                        bandlimit_kernel=True, device=dev)
         self.asm_prop2detector = ASM_prop(z_distance=50 * mm, bandlimit_type='exact', padding_scale=2,
                                           bandlimit_kernel=True, device=dev)
+        # wavelength / spacing tensors made once (fp32 casts of ElectricField.check_*): building the
+        # input field per step then copies nothing host->device, so a step can be graph-captured
+        self._tmpl = ElectricField(data=torch.zeros(1, 1, 1, 1, dtype=torch.complex64), wavelengths=wavelengths,
+                                   spacing=input_dxy, device=dev)
 
     def encode_object(self, u):
         """Plane wave times the object amplitude ``u`` [B, 1, H, W] -> ASM 50 mm -> aperture (nb :171-190)."""
         u = u.to(self.device)
-        field = ElectricField(data=u.to(torch.complex64), wavelengths=self.wavelengths, spacing=self.input_dxy,
-                              device=self.device)
+        field = ElectricField(data=u.to(torch.complex64), wavelengths=self._tmpl.wavelengths,
+                              spacing=self._tmpl.spacing, device=self.device)._adopt_host(self._tmpl)
         return self.aperture(self.asm_prop2layer(field))
 
     def forward(self, u, iter_frac=None, chained=False):
@@ -94,6 +99,158 @@ class DONN(nn.Module):
             field = self.aperture(field)
         field = self.does[-1](field if chained else inputs, iter_frac)
         return self.asm_prop2detector(field)
+
+
+def detector_targets(num_classes=10, shape=(100, 100), det=10, device=None):
+    """Per-class target intensity images [num_classes, 1, H, W] (float32): ones inside the class's
+    det x det detector square, zeros elsewhere.  The detectors sit in three rows (3, 4, 3) centred
+    in the plane, the usual 10-class DONN readout.
+
+    The reference notebook's label-generator and training cells are empty
+    (experiment_DONN_3_layers.ipynb, sections 3-5), so this layout is this framework's choice;
+    the loss it feeds is the reference's QAT loss, MSE(normalize(|E|^2), target)
+    (experiment_four_focal_spots.ipynb:336-370, utils/Helper_Functions.py:185-193)."""
+    H, W = shape
+    if num_classes > 10:
+        raise ValueError("detector_targets lays out at most 10 detectors")
+    rows = [(H * 0.25, 3), (H * 0.5, 4), (H * 0.75, 3)]
+    centres = []
+    for yc, n in rows:
+        for j in range(n):
+            centres.append((yc, W * (j + 1) / (n + 1)))
+    t = torch.zeros(num_classes, 1, H, W, dtype=torch.float32)
+    for k in range(num_classes):
+        yc, xc = centres[k]
+        y0, x0 = int(round(yc - det / 2)), int(round(xc - det / 2))
+        t[k, 0, max(y0, 0):y0 + det, max(x0, 0):x0 + det] = 1.0
+    dev = device or torch.device("cuda" if torch.cuda.is_available() else "cpu")
+    return t.to(dev)
+
+
+class DONNTrainer:
+    """Data-parallel DONN training step: forward of this rank's share of
+    the batch, loss = MSE(normalize(|E|^2), per-sample detector target), backward through the
+    HIP adjoint kernels, ONE flat all-reduce of the three layers' weight gradients (120 KB at
+    100^2; RCCL over xGMI on the GPU, gloo in the CPU tests), Adam.
+
+    ``chained=False`` keeps the notebook's forward (every layer modulates the encoded input, so
+    only the last layer receives a gradient; the others contribute zeros to the all-reduce).
+    ``graph=True`` captures the step as HIP graphs per schedule phase (qat.QATTrainer's scheme):
+    the batch and its targets are copied into static device buffers before each replay.
+    """
+
+    def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True):
+        from quantizationawarethzdoe_amd.qat import GradientAllReduce
+        self.model = model
+        self.targets = targets.to(model.device).float().contiguous()
+        self.max_itrs = max_itrs
+        self.graph = graph
+        self.chained = chained
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph)
+        self.allreduce = GradientAllReduce(self.params, group=group)
+        self.itr = 0
+        self._graphs = {}
+        self._static = None
+        if graph:
+            self.dyn = torch.zeros(3, dtype=torch.float32, device=model.device)
+            for d in model.does:
+                d._dyn = self.dyn
+
+    def _loss(self, u, target, frac):
+        from quantizationawarethzdoe_amd.optics import intensity_mse
+        out = self.model(u, frac, chained=self.chained)
+        return intensity_mse(out.data, target)
+
+    def step(self, u, labels, iter_frac=None):
+        """One iteration on images ``u`` [B, 1, H, W] (float, this rank's share) and int64 ``labels`` [B]."""
+        frac = self.itr / self.max_itrs if iter_frac is None else iter_frac
+        u = u.to(self.model.device, torch.float32)
+        target = self.targets.index_select(0, labels.to(self.model.device))
+        if self.graph:
+            loss = self._graph_step(u, target, frac)
+        else:
+            loss = self._loss(u, target, frac)
+            self.optimizer.zero_grad(set_to_none=False)
+            loss.backward()
+            self.allreduce()
+            self.optimizer.step()
+        self.itr += 1
+        return loss
+
+    # -- graph path ----------------------------------------------------------------------------
+    def _pack(self):
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            if p.grad is None:
+                self.allreduce.flat[off:off + k].zero_()
+            else:
+                self.allreduce.flat[off:off + k].copy_(p.grad.reshape(-1))
+            off += k
+
+    def _unpack(self):
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            if p.grad is not None:
+                p.grad.copy_(self.allreduce.flat[off:off + k].view_as(p))
+            off += k
+
+    def _capture(self, frac):
+        su, st = self._static
+        p0 = [p.detach().clone() for p in self.params]
+        st0 = {id(p): {k: v.clone() for k, v in self.optimizer.state[p].items() if torch.is_tensor(v)}
+               for p in self.params if p in self.optimizer.state}
+        side = torch.cuda.Stream(device=self.model.device)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):  # allocator, autograd and Adam's lazy state, outside the capture
+                self.optimizer.zero_grad(set_to_none=True)
+                self._loss(su, st, frac).backward()
+                self.optimizer.step()
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        with torch.no_grad():  # the warm-up must not move the training trajectory
+            for p, v in zip(self.params, p0):
+                p.copy_(v)
+            for p in self.params:
+                saved = st0.get(id(p))
+                for k, v in self.optimizer.state.get(p, {}).items():
+                    if torch.is_tensor(v):
+                        v.copy_(saved[k]) if saved is not None else v.zero_()
+        self.optimizer.zero_grad(set_to_none=True)
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            loss = self._loss(su, st, frac)
+            loss.backward()
+            if self.allreduce.world > 1:
+                self._pack()
+        with torch.cuda.graph(g_opt):
+            if self.allreduce.world > 1:
+                self._unpack()
+            self.optimizer.step()
+        return g_fb, g_opt, loss
+
+    def _graph_step(self, u, target, frac):
+        if self._static is None or self._static[0].shape != u.shape:
+            self._static = (torch.empty_like(u), torch.empty_like(target))
+            self._graphs = {}
+        su, st = self._static
+        su.copy_(u)
+        st.copy_(target)
+        lead = self.model.does[0]
+        phase = lead._graph_phase(frac)
+        self.dyn.copy_(torch.tensor(list(lead._dyn_values(frac)), dtype=torch.float32))
+        if phase not in self._graphs:
+            self._graphs[phase] = self._capture(frac)
+        g_fb, g_opt, loss = self._graphs[phase]
+        g_fb.replay()
+        if self.allreduce.world > 1:
+            dist.all_reduce(self.allreduce.flat, op=dist.ReduceOp.SUM, group=self.allreduce.group)
+            self.allreduce.flat.mul_(1.0 / self.allreduce.world)
+        g_opt.replay()
+        return loss
 
 
 def read_idx_images(path, count=None):

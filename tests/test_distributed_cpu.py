@@ -57,6 +57,20 @@ def test_gradient_allreduce_gloo_world2():
     assert all(ok and has for _, ok, has in res), res
 
 
+def test_donn_detector_targets_and_cpu_refusal():
+    """cfg5: ten disjoint det x det detector targets; the trainer refuses a CPU model loudly."""
+    from quantizationawarethzdoe_amd import donn
+    t = donn.detector_targets(device=torch.device("cpu"))
+    assert t.shape == (10, 1, 100, 100)
+    assert all(float(t[k].sum()) == 100.0 for k in range(10))
+    assert float(t.sum(0).max()) == 1.0
+    model = donn.DONN(device=torch.device("cpu"))
+    tr = donn.DONNTrainer(model, t)
+    assert tr.allreduce.world == 1 and sum(p.numel() for p in tr.params) == 3 * 100 * 100
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        tr.step(torch.rand(2, 1, 100, 100), torch.tensor([1, 2]))
+
+
 def test_plane_sharding_covers_every_plane_once():
     from bench import shard_planes
     for n_planes in (1, 7, 64, 512):
