@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
       const int c = band_col(j, PN, a.J, a.ncols);
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
-    fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
         const int r = j - a.out_r0;
         if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
       };
-      fft_pow2_io<true, PN, TT, false, false, false>(lds, twl, tz, ld1, sv1);
+      fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
       return;
     }
     // The evanescent and band-limit masks are monotone in |m_x| (every fp32 operation of
@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
         const int r = j - a.out_r0;
         if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v;
       };
-      fft_pow2_io<true, PN, TT, false, false, false>(lds, twl, tz, ld1, sv1);
+      fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
     }
   } else {
     for (int i = tid; i < Ph; i += nt) {
@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
       const int w = j - a.out_c0;
       if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
     };
-    fft_pow2_run<true, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<true, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);
@@ -434,7 +434,7 @@ __global__ void __launch_bounds__(1024) rsc_k_rows(float2* __restrict__ TK, FftP
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     auto ld = [&](int, int, int j) { return load(j); };
     auto sv = [&](int, int, int j, float2 v) { store(j, v); };
-    fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < k.Pw; j += nt) lds[padx(j)] = load(j);
     __syncthreads();
@@ -456,7 +456,7 @@ __global__ void __launch_bounds__(1024) rsc_k_cols(const float2* __restrict__ TK
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), ph.tw, tid, nt);
     auto ld = [&](int, int, int i) { return col[(size_t)i * CB]; };
     auto sv = [&](int, int, int i, float2 v) { dst[i] = v; };
-    fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int i = tid; i < k.Ph; i += nt) lds[padx(i)] = col[(size_t)i * CB];
     __syncthreads();
@@ -478,8 +478,8 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), p.tw, tid, nt);
     auto ld = [&](int, int, int j) { return in[base + j]; };
     auto sv = [&](int, int, int j, float2 v) { out[base + j] = v; };
-    if (inverse) fft_pow2_run<true, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
-    else fft_pow2_run<false, PN, Geo<PN>::T, false>(lds, twl, tid, ld, sv);
+    if (inverse) fft_pow2_run<true, PN, Geo<PN>::T, FFT_TAIL>(lds, twl, tid, ld, sv);
+    else fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];
     __syncthreads();

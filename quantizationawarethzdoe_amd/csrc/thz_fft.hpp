@@ -500,8 +500,24 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
   }
 }
 
-// Radix schedule of a power-of-two N: 16s plus one remainder radix b in {2,4,8} (or none),
-// placed last (SMALL_FIRST = false) or first (true).
+// Radix schedule of a power-of-two N: 16s plus one remainder radix b in {2,4,8} (or none).
+// MODE 0: remainder last; 1: remainder first; 2 (FFT_TAIL): a radix-2 remainder merged with the
+// last radix-16 stage into one radix-32 stage on lane pairs (stage_r32_pair_last) -- one LDS
+// exchange and its barriers fewer; other remainders as MODE 0.  (The register hand-off between
+// a MODE-0 forward and a MODE-1 inverse, as in the CZT kernels, needs MODE 0 / 1.)
+// Measured on cfg2 (8192 points): the column pass (complex image, 4 waves/SIMD) runs 2.69 -> 2.32
+// ms per 32 planes with the pair tail; the 64-VGPR split-image row passes run slower with it
+// (K3 2.19 -> 2.62 ms: the tail spills at 64 VGPRs and its half-masked crop stores double the
+// store instructions), so they keep MODE 0 (FFT_TAIL_ROWS).  fft_rows_kernel (diagnostics) runs
+// the split-image pair tail so that form stays tested.
+#ifndef THZ_PAIR32
+#define THZ_PAIR32 1
+#endif
+#ifndef THZ_PAIR32_ROWS
+#define THZ_PAIR32_ROWS 0
+#endif
+constexpr int FFT_TAIL = THZ_PAIR32 ? 2 : 0;
+constexpr int FFT_TAIL_ROWS = THZ_PAIR32_ROWS ? 2 : 0;
 template <int N>
 struct Pow2Sched {
   static constexpr int log2n() {
@@ -515,12 +531,99 @@ struct Pow2Sched {
   static constexpr int NS16 = LOG / LV;  // full-radix (V) stages
   static constexpr int REM = 1 << (LOG % LV);
   static constexpr int NST = NS16 + (REM > 1 ? 1 : 0);
-  static constexpr int radix(int s, bool small_first) {
+  static constexpr bool PAIR = REM == 2 && V == 16 && NS16 >= 2;
+  static constexpr int nst(int mode) { return mode == 2 && PAIR ? NS16 : NST; }
+  static constexpr int radix(int s, int mode) {
     if (REM == 1) return V;
-    if (small_first) return s == 0 ? REM : V;
+    if (mode == 1) return s == 0 ? REM : V;
+    if (mode == 2 && PAIR) return s == NS16 - 1 ? 32 : V;
     return s == NST - 1 ? REM : V;
   }
 };
+
+// ---------------------------------------------------------------------------------------------
+// Radix-32 last stage on lane pairs (MODE 2; L = N/32 butterflies, k = i, L R = N).  Butterfly i
+// runs on lanes l and l + 32 of one wave (i = 32 wave + l mod 32, e = l / 32); lane e holds the
+// inputs x_{2s+e}, s < 16, and forms A_e = w^{e i} DFT16_s(x_{2s+e} w^{2 s i}).  Then
+// X_q = A_0[q] + w32^q A_1[q] and X_{q+16} = A_0[q] - w32^q A_1[q]: one v_permlane32_swap per
+// dword pairs (A_0[q], A_1[q]) for q < 8 in the low half-wave and for q >= 8 in the high half,
+// and each lane finishes 8 radix-2 butterflies -- no LDS exchange and no barrier for the
+// radix-2 step.  Reads of this stage (x[i + (2s+e) L]) are conflict-free on the L = N/512
+// exchange images: every 32-lane group shares e and covers 32 consecutive i.
+// ---------------------------------------------------------------------------------------------
+__host__ __device__ constexpr int pair_i(int tid) { return ((tid >> 6) << 5) | (tid & 31); }
+
+__device__ __forceinline__ void swap_halves(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(b), false, false);
+  a = __int_as_float(r[0]);
+  b = __int_as_float(r[1]);
+}
+
+template <bool INV, int N, class Tw, class Sv>
+__device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float2 (&x)[16], Sv& sv) {
+  constexpr int L = N / 32;
+  // exp(-2 pi i q / 32), q < 8
+  constexpr float C32C[8] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                             0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                             0.19509032201612826785f};
+  constexpr float C32S[8] = {0.0f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
+                             0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
+                             0.98078528040323044913f};
+  const int e = (tid >> 5) & 1, i = pair_i(tid);
+  {
+    // w^{2 i s}: the powers 1, 2, 4, 8 from the table, the rest by the products of
+    // twiddle_powers, each formed next to its use (short live ranges: the row kernels run at 64
+    // VGPRs)
+    const float2 w1 = twat(tw, 2 * i), w2 = twat(tw, 4 * i), w4 = twat(tw, 8 * i), w8 = twat(tw, 16 * i);
+    const float2 w3 = cmul(w1, w2), w5 = cmul(w1, w4), w6 = cmul(w2, w4), w7 = cmul(w3, w4);
+    x[1] = cmul_tw<INV>(x[1], w1);
+    x[2] = cmul_tw<INV>(x[2], w2);
+    x[3] = cmul_tw<INV>(x[3], w3);
+    x[4] = cmul_tw<INV>(x[4], w4);
+    x[5] = cmul_tw<INV>(x[5], w5);
+    x[6] = cmul_tw<INV>(x[6], w6);
+    x[7] = cmul_tw<INV>(x[7], w7);
+    x[8] = cmul_tw<INV>(x[8], w8);
+    x[9] = cmul_tw<INV>(x[9], cmul(w1, w8));
+    x[10] = cmul_tw<INV>(x[10], cmul(w2, w8));
+    x[11] = cmul_tw<INV>(x[11], cmul(w3, w8));
+    x[12] = cmul_tw<INV>(x[12], cmul(w4, w8));
+    x[13] = cmul_tw<INV>(x[13], cmul(w5, w8));
+    x[14] = cmul_tw<INV>(x[14], cmul(w6, w8));
+    x[15] = cmul_tw<INV>(x[15], cmul(w7, w8));
+  }
+  dftR<16, INV>(x);
+  // the odd lane's common input factor w^{i} is left out above and applied after the swap
+  // (linearity), where every lane holds an odd-lane DFT output of the same butterfly
+  const float2 wi = twat(tw, i);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float2 a = x[q], b = x[q + 8];
+    swap_halves(a.x, b.x);
+    swap_halves(a.y, b.y);
+    // now (a, w^i b) = (A_0[q + 8e], A_1[q + 8e]); w32^{q + 8e} = w32^q (-+i)^e
+    float2 t = cmul_tw<INV>(b, q == 0 ? wi : cmul(wi, make_float2(C32C[q], -C32S[q])));
+    const float2 tr = mul_mi<INV>(t);
+    t = e ? tr : t;
+    sv(0, q, i + (q + 8 * e) * L, cadd(a, t));
+    sv(0, q + 16, i + (q + 8 * e + 16) * L, csub(a, t));
+    // keep each q's swap / multiply next to its (predicated) stores: hoisting them all above
+    // the first store region spills the 64-VGPR row kernels
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// The pair stage reads x[i + (2s+e) L] at base lay(i + e L) plus lay(2 s L) - lay(0): true for
+// the layouts used when the per-lane part of the index never carries into the padded bits.
+template <class F>
+__host__ __device__ constexpr bool pair_offsets_ok(F lay, int N) {
+  const int L = N / 32;
+  for (int e = 0; e < 2; ++e)
+    for (int i = 0; i < L; i += L - 1)
+      for (int s = 0; s < 16; ++s)
+        if (lay(i + e * L + 2 * s * L) - lay(i + e * L) != lay(2 * s * L) - lay(0)) return false;
+  return true;
+}
 
 struct NoIO {
   __device__ float2 operator()(int, int, int) const { return make_float2(0.f, 0.f); }
@@ -529,19 +632,32 @@ struct NoIO {
 
 // Stages S .. NST-1 of a power-of-two transform.  Stage 0 reads through ld unless
 // FIRST_LDS; the final stage writes through sv unless LAST_LDS.
-template <bool INV, int N, int T, bool SMALL_FIRST, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1,
+template <bool INV, int N, int T, int MODE, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1,
           class Tw, class Ld, class Sv>
 __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
   using P = Pow2Sched<N>;
-  if constexpr (S < P::NST) {
-    constexpr int R = P::radix(S, SMALL_FIRST);
+  constexpr int NS = P::nst(MODE);
+  if constexpr (S < NS) {
+    constexpr int R = P::radix(S, MODE);
     constexpr bool IN_LDS = S > 0 || FIRST_LDS;
-    constexpr bool OUT_LDS = S < P::NST - 1 || LAST_LDS;
+    constexpr bool OUT_LDS = S < NS - 1 || LAST_LDS;
     // image layouts: the previous stage's (L / its radix); natural-order padx at the two ends
-    constexpr int LIN = S == 0 ? 1 : L / P::radix(S - 1, SMALL_FIRST);
-    constexpr int LOUT = S == P::NST - 1 ? 1 : L;
-    stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv);
-    fft_pow2_io<INV, N, T, SMALL_FIRST, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
+    constexpr int LIN = S == 0 ? 1 : L / P::radix(S - 1, MODE);
+    constexpr int LOUT = S == NS - 1 ? 1 : L;
+    if constexpr (R == 32) {
+      static_assert(S > 0 && S == NS - 1 && !LAST_LDS && T == N / 16, "pair stage: last, reading LDS");
+      static_assert(pair_offsets_ok([](int j) { return c64_lay<LIN>(j); }, N), "pair-stage offsets");
+      constexpr int LP = N / 32;
+      const int e = (tid >> 5) & 1;
+      const float2* src = lds + c64_lay<LIN>(pair_i(tid) + e * LP);
+      float2 x[16];
+#pragma unroll
+      for (int s = 0; s < 16; ++s) x[s] = src[c64_lay<LIN>(2 * s * LP) - c64_lay<LIN>(0)];
+      stage_r32_pair_last<INV, N>(tw, tid, x, sv);
+    } else {
+      stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv);
+      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
+    }
   }
 }
 
@@ -593,14 +709,14 @@ __host__ __device__ constexpr int split_c(int L) { return L == 1 ? 1 : (L <= 16 
 template <int L>
 __host__ __device__ constexpr int split_lay(int j) { return j + split_c(L) * (j >> split_sh(L)); }
 
-template <bool INV, int N, int T, bool SMALL_FIRST, int S = 0, int L = 1, class Tw, class In, class Sv>
+template <bool INV, int N, int T, int MODE, int S = 0, int L = 1, class Tw, class In, class Sv>
 __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int tid, In& in, Sv& sv) {
   using P = Pow2Sched<N>;
-  constexpr int R = P::radix(S, SMALL_FIRST);
+  constexpr int R = P::radix(S, MODE);
   constexpr int MB = N / R / T;
   float2 v[MB][R];
   stage_core<R, INV, N, L, T>(tw, tid, in, v);
-  if constexpr (S == P::NST - 1) {
+  if constexpr (S == P::nst(MODE) - 1) {
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
       const int i = tid + m * T;
@@ -608,11 +724,15 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
       for (int r = 0; r < R; ++r) sv(m, r, i + r * L, v[m][r]);  // last stage: L R = N, k = i
     }
   } else {
-    constexpr int R2 = P::radix(S + 1, SMALL_FIRST);
+    constexpr int R2 = P::radix(S + 1, MODE);
+    constexpr bool PAIR = R2 == 32;  // next: the radix-32 lane-pair last stage
     constexpr int NB2 = N / R2;
-    constexpr int MB2 = NB2 / T;
+    constexpr int MB2 = PAIR ? 1 : NB2 / T;
+    constexpr int RR2 = PAIR ? 16 : R2;
     static_assert(split_lay<L>(N - 1) < 2 * lds_split_f2(N), "split layout exceeds the LDS image");
-    float2 nx[MB2][R2];
+    static_assert(!PAIR || (T == N / 16 && S + 2 == P::nst(MODE)), "pair stage layout");
+    static_assert(!PAIR || pair_offsets_ok([](int j) { return split_lay<L>(j); }, N), "pair-stage offsets");
+    float2 nx[MB2][RR2];
     // output element j = (i - k) R + k + r L of this stage -> input i2 + r2 NB2 of the next; the
     // per-r address offsets are those of thread 0 (constant over threads for these layouts)
 #pragma unroll
@@ -629,19 +749,34 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
           dst[split_lay<L>(j0 + r * L) - split_lay<L>(j0)] = part ? v[m][r].y : v[m][r].x;
       }
       __syncthreads();
+      if constexpr (PAIR) {
+        constexpr int LP = N / 32;
+        const float* src = lds + split_lay<L>(pair_i(tid) + ((tid >> 5) & 1) * LP);
 #pragma unroll
-      for (int m = 0; m < MB2; ++m) {
-        const float* src = lds + split_lay<L>(tid + m * T);
+        for (int s = 0; s < 16; ++s) {
+          const float x = src[split_lay<L>(2 * s * LP) - split_lay<L>(0)];
+          if (part) nx[0][s].y = x;
+          else nx[0][s].x = x;
+        }
+      } else {
 #pragma unroll
-        for (int r = 0; r < R2; ++r) {
-          const float x = src[split_lay<L>(m * T + r * NB2) - split_lay<L>(m * T)];
-          if (part) nx[m][r].y = x;
-          else nx[m][r].x = x;
+        for (int m = 0; m < MB2; ++m) {
+          const float* src = lds + split_lay<L>(tid + m * T);
+#pragma unroll
+          for (int r = 0; r < R2; ++r) {
+            const float x = src[split_lay<L>(m * T + r * NB2) - split_lay<L>(m * T)];
+            if (part) nx[m][r].y = x;
+            else nx[m][r].x = x;
+          }
         }
       }
     }
-    auto in2 = [&](int m, int r, int) { return nx[m][r]; };
-    fft_pow2_split_io<INV, N, T, SMALL_FIRST, S + 1, L * R>(lds, tw, tid, in2, sv);
+    if constexpr (PAIR) {
+      stage_r32_pair_last<INV, N>(tw, tid, nx[0], sv);
+    } else {
+      auto in2 = [&](int m, int r, int) { return nx[m][r]; };
+      fft_pow2_split_io<INV, N, T, MODE, S + 1, L * R>(lds, tw, tid, in2, sv);
+    }
   }
 }
 
@@ -651,12 +786,12 @@ template <int N>
 __device__ __forceinline__ float2* tw_slot(float2* lds) {
   return lds + (THZ_SPLIT ? lds_split_f2(N) : lds_floats2(N));
 }
-template <bool INV, int N, int T, bool SMALL_FIRST, class Tw, class Ld, class Sv>
+template <bool INV, int N, int T, int MODE, class Tw, class Ld, class Sv>
 __device__ __forceinline__ void fft_pow2_run(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
 #if THZ_SPLIT
-  fft_pow2_split_io<INV, N, T, SMALL_FIRST>(reinterpret_cast<float*>(lds), tw, tid, ld, sv);
+  fft_pow2_split_io<INV, N, T, MODE>(reinterpret_cast<float*>(lds), tw, tid, ld, sv);
 #else
-  fft_pow2_io<INV, N, T, SMALL_FIRST, false, false>(lds, tw, tid, ld, sv);
+  fft_pow2_io<INV, N, T, MODE, false, false>(lds, tw, tid, ld, sv);
 #endif
 }
 
