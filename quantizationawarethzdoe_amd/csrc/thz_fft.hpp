@@ -28,7 +28,10 @@ constexpr int FFT_MAX_STAGES = 24;
 #endif
 // Split-exchange row kernels of 8192 / 16384 points: the LDS image allows 8 waves / SIMD, so
 // hold them to 64 VGPRs (the smaller sizes are LDS-limited below 8 and would only spill).
-__host__ __device__ constexpr int row_waves_per_eu(int n) { return THZ_SPLIT && n >= 8192 ? 8 : 1; }
+#ifndef THZ_ROW_WPE
+#define THZ_ROW_WPE 8
+#endif
+__host__ __device__ constexpr int row_waves_per_eu(int n) { return THZ_SPLIT && n >= 8192 ? THZ_ROW_WPE : 1; }
 #define THZ_ROW_ATTR __attribute__((amdgpu_waves_per_eu(row_waves_per_eu(PN))))
 constexpr int FFT_MAXV = 16;  // complex values held per thread per stage (N <= 16 * threads)
 #ifndef THZ_PV
@@ -546,7 +549,7 @@ struct Pow2Sched {
 // runs on lanes l and l + 32 of one wave (i = 32 wave + l mod 32, e = l / 32); lane e holds the
 // inputs x_{2s+e}, s < 16, and forms A_e = w^{e i} DFT16_s(x_{2s+e} w^{2 s i}).  Then
 // X_q = A_0[q] + w32^q A_1[q] and X_{q+16} = A_0[q] - w32^q A_1[q]: one v_permlane32_swap per
-// dword pairs (A_0[q], A_1[q]) for q < 8 in the low half-wave and for q >= 8 in the high half,
+// dword pairs (A_0[q], A_1[q]) for even q in the low half-wave and for odd q in the high half,
 // and each lane finishes 8 radix-2 butterflies -- no LDS exchange and no barrier for the
 // radix-2 step.  Reads of this stage (x[i + (2s+e) L]) are conflict-free on the L = N/512
 // exchange images: every 32-lane group shares e and covers 32 consecutive i.
@@ -562,13 +565,17 @@ __device__ __forceinline__ void swap_halves(float& a, float& b) {
 template <bool INV, int N, class Tw, class Sv>
 __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float2 (&x)[16], Sv& sv) {
   constexpr int L = N / 32;
-  // exp(-2 pi i q / 32), q < 8
-  constexpr float C32C[8] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
-                             0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
-                             0.19509032201612826785f};
-  constexpr float C32S[8] = {0.0f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
-                             0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
-                             0.98078528040323044913f};
+  // exp(-2 pi i q / 32) = (C32C[q], -C32S[q]), q < 16
+  constexpr float C32C[16] = {1.0f, 0.98078528040323044913f, 0.92387953251128675613f, 0.83146961230254523708f,
+                              0.70710678118654752440f, 0.55557023301960222474f, 0.38268343236508977173f,
+                              0.19509032201612826785f, 0.0f, -0.19509032201612826785f, -0.38268343236508977173f,
+                              -0.55557023301960222474f, -0.70710678118654752440f, -0.83146961230254523708f,
+                              -0.92387953251128675613f, -0.98078528040323044913f};
+  constexpr float C32S[16] = {0.0f, 0.19509032201612826785f, 0.38268343236508977173f, 0.55557023301960222474f,
+                              0.70710678118654752440f, 0.83146961230254523708f, 0.92387953251128675613f,
+                              0.98078528040323044913f, 1.0f, 0.98078528040323044913f, 0.92387953251128675613f,
+                              0.83146961230254523708f, 0.70710678118654752440f, 0.55557023301960222474f,
+                              0.38268343236508977173f, 0.19509032201612826785f};
   const int e = (tid >> 5) & 1, i = pair_i(tid);
   {
     // w^{2 i s}: the powers 1, 2, 4, 8 from the table, the rest by the products of
@@ -593,21 +600,24 @@ __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float
     x[15] = cmul_tw<INV>(x[15], cmul(w7, w8));
   }
   dftR<16, INV>(x);
-  // the odd lane's common input factor w^{i} is left out above and applied after the swap
-  // (linearity), where every lane holds an odd-lane DFT output of the same butterfly
+  // The odd lane's common input factor w^{i} is left out above and applied after the swap
+  // (linearity).  The swap pairs registers (2p, 2p + 1): the low half-wave then holds
+  // (A_0[q], A_1[q]) for q = 2p and the high half for q = 2p + 1, so a lane's outputs
+  // q + 16 e' (e' = 0, 1) sit at the same place relative to a centred crop in both halves and
+  // every store of a cropped row is all-lanes or none.
   const float2 wi = twat(tw, i);
+  const float2 f = e ? cmul(wi, make_float2(C32C[1], -C32S[1])) : wi;  // w^i w32^e
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    float2 a = x[q], b = x[q + 8];
+  for (int p = 0; p < 8; ++p) {
+    float2 a = x[2 * p], b = x[2 * p + 1];
     swap_halves(a.x, b.x);
     swap_halves(a.y, b.y);
-    // now (a, w^i b) = (A_0[q + 8e], A_1[q + 8e]); w32^{q + 8e} = w32^q (-+i)^e
-    float2 t = cmul_tw<INV>(b, q == 0 ? wi : cmul(wi, make_float2(C32C[q], -C32S[q])));
-    const float2 tr = mul_mi<INV>(t);
-    t = e ? tr : t;
-    sv(0, q, i + (q + 8 * e) * L, cadd(a, t));
-    sv(0, q + 16, i + (q + 8 * e + 16) * L, csub(a, t));
-    // keep each q's swap / multiply next to its (predicated) stores: hoisting them all above
+    // now (a, w^i b) = (A_0[q], A_1[q]), q = 2p + e;  w32^q = w32^{2p} w32^e
+    const float2 t = cmul_tw<INV>(b, p == 0 ? f : cmul(f, make_float2(C32C[2 * p], -C32S[2 * p])));
+    const int q = 2 * p + e;
+    sv(0, 2 * p, i + q * L, cadd(a, t));
+    sv(0, 2 * p + 16, i + (q + 16) * L, csub(a, t));
+    // keep each p's swap / multiply next to its (predicated) stores: hoisting them all above
     // the first store region spills the 64-VGPR row kernels
     __builtin_amdgcn_sched_barrier(0);
   }
