@@ -1,6 +1,8 @@
 set -o pipefail
 mkdir -p gpurun_out
-bash scripts/gpu_step.sh 400 gpurun_out/donn_tests.log python -u -m pytest tests/test_donn_train_gpu.py tests/test_optics_qat_gpu.py -x -v --timeout 120 --timeout-method thread &&
-tail -3 gpurun_out/donn_tests.log &&
-bash scripts/gpu_step.sh 400 gpurun_out/bench_sec.log python bench.py --no-cpu-baseline &&
-tail -2 gpurun_out/bench_sec.log
+bash scripts/gpu_step.sh 600 gpurun_out/gpu_tests.log python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread &&
+tail -2 gpurun_out/gpu_tests.log &&
+bash scripts/gpu_step.sh 600 gpurun_out/bench.log python bench.py &&
+tail -1 gpurun_out/bench.log | cut -c1-300 &&
+bash scripts/profile_asm.sh gpurun_out/prof_r01 &&
+REPS=2 bash scripts/exp_multi.sh default base

@@ -181,7 +181,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
       const int c = band_col(j, PN, a.J, a.ncols);
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
-    fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
@@ -378,6 +378,25 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
     // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
     // frequencies), a multiple of CBU: the blocked address is then base(c0) + delta_q*Hout,
     // one add per element instead of the full blk_u() per element.
+    if constexpr (FFT_ROWS == 3 && Pow2Sched<PN>::PAIR) {
+      // lane-pair radix-32 first stage: lane e of butterfly i reads j = i + (16 e + q) PN/32, band
+      // column c0 + q PN/32 with c0 = i + J - e PN/2 (the upper half holds the negative
+      // frequencies); floor division by CBU keeps the blocked address affine in q for c0 < 0
+      constexpr int LP = PN / 32;
+      static_assert(CBU == 4 && LP % CBU == 0, "pair-first gather offsets");
+      const int c0 = pair_i(tid) + a.J - ((tid >> 5) & 1) * (PN / 2);
+      const float2* base = src + ((long)(c0 >> 2) * a.Hout + r) * CBU + (c0 & (CBU - 1));
+      auto ld = [&](int, int q, int) {
+        if ((unsigned)(c0 + q * LP) >= (unsigned)a.ncols) return make_float2(0.f, 0.f);
+        return base[(long)(q * LP) * a.Hout];
+      };
+      auto sv = [&](int, int, int j, float2 v) {
+        const int w = j - a.out_c0;
+        if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
+      };
+      fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
+      return;
+    }
     constexpr int NB0 = PN / pow2_v(PN);  // first stage: radix pow2_v, L = 1
     static_assert(NB0 % CBU == 0, "band offsets must be whole U blocks");
     static_assert(Geo<PN>::T == NB0, "one first-stage butterfly per thread: i = tid");
@@ -392,7 +411,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
       const int w = j - a.out_c0;
       if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
     };
-    fft_pow2_run<true, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS == 3 ? 0 : FFT_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);
@@ -434,7 +453,7 @@ __global__ void __launch_bounds__(1024) rsc_k_rows(float2* __restrict__ TK, FftP
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     auto ld = [&](int, int, int j) { return load(j); };
     auto sv = [&](int, int, int j, float2 v) { store(j, v); };
-    fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < k.Pw; j += nt) lds[padx(j)] = load(j);
     __syncthreads();
@@ -456,7 +475,7 @@ __global__ void __launch_bounds__(1024) rsc_k_cols(const float2* __restrict__ TK
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), ph.tw, tid, nt);
     auto ld = [&](int, int, int i) { return col[(size_t)i * CB]; };
     auto sv = [&](int, int, int i, float2 v) { dst[i] = v; };
-    fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int i = tid; i < k.Ph; i += nt) lds[padx(i)] = col[(size_t)i * CB];
     __syncthreads();
@@ -478,7 +497,7 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), p.tw, tid, nt);
     auto ld = [&](int, int, int j) { return in[base + j]; };
     auto sv = [&](int, int, int j, float2 v) { out[base + j] = v; };
-    if (inverse) fft_pow2_run<true, PN, Geo<PN>::T, FFT_TAIL>(lds, twl, tid, ld, sv);
+    if (inverse) fft_pow2_run<true, PN, Geo<PN>::T, 3>(lds, twl, tid, ld, sv);
     else fft_pow2_run<false, PN, Geo<PN>::T, FFT_TAIL>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < p.n; j += nt) lds[padx(j)] = in[base + j];

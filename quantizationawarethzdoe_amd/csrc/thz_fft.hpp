@@ -509,18 +509,22 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
 // exchange and its barriers fewer; other remainders as MODE 0.  (The register hand-off between
 // a MODE-0 forward and a MODE-1 inverse, as in the CZT kernels, needs MODE 0 / 1.)
 // Measured on cfg2 (8192 points): the column pass (complex image, 4 waves/SIMD) runs 2.69 -> 2.32
-// ms per 32 planes with the pair tail; the 64-VGPR split-image row passes run slower with it
-// (K3 2.19 -> 2.62 ms: the tail spills at 64 VGPRs and its half-masked crop stores double the
-// store instructions), so they keep MODE 0 (FFT_TAIL_ROWS).  fft_rows_kernel (diagnostics) runs
-// the split-image pair tail so that form stays tested.
+// ms per 32 planes with the pair tail (MODE 2).  The 64-VGPR split-image row passes do not gain
+// from either lane-pair form: the tail spills at 64 VGPRs (K3 2.19 -> 2.62 ms); the head (MODE 3,
+// one LDS exchange fewer, no input twiddles) leaves a full radix-16 last stage whose twiddles and
+// cropped stores spill at 64 VGPRs (3.31 ms) and run 2.32 ms at 7 waves/SIMD without spills --
+// so the row passes are not LDS-exchange-bound and keep MODE 0 (THZ_ROWS_MODE).  fft_rows_kernel
+// (diagnostics) runs MODE 2 forward and MODE 3 inverse so both split-image forms stay tested.
 #ifndef THZ_PAIR32
 #define THZ_PAIR32 1
 #endif
-#ifndef THZ_PAIR32_ROWS
-#define THZ_PAIR32_ROWS 0
+// Row passes (split image): THZ_ROWS_MODE 3 puts the lane-pair radix 32 first (decimation in
+// frequency), 2 last, 0 neither (the default, measured above).
+#ifndef THZ_ROWS_MODE
+#define THZ_ROWS_MODE 0
 #endif
 constexpr int FFT_TAIL = THZ_PAIR32 ? 2 : 0;
-constexpr int FFT_TAIL_ROWS = THZ_PAIR32_ROWS ? 2 : 0;
+constexpr int FFT_ROWS = THZ_ROWS_MODE;
 template <int N>
 struct Pow2Sched {
   static constexpr int log2n() {
@@ -535,11 +539,12 @@ struct Pow2Sched {
   static constexpr int REM = 1 << (LOG % LV);
   static constexpr int NST = NS16 + (REM > 1 ? 1 : 0);
   static constexpr bool PAIR = REM == 2 && V == 16 && NS16 >= 2;
-  static constexpr int nst(int mode) { return mode == 2 && PAIR ? NS16 : NST; }
+  static constexpr int nst(int mode) { return mode >= 2 && PAIR ? NS16 : NST; }
   static constexpr int radix(int s, int mode) {
     if (REM == 1) return V;
     if (mode == 1) return s == 0 ? REM : V;
     if (mode == 2 && PAIR) return s == NS16 - 1 ? 32 : V;
+    if (mode == 3 && PAIR) return s == 0 ? 32 : V;
     return s == NST - 1 ? REM : V;
   }
 };
@@ -621,6 +626,42 @@ __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float
     // the first store region spills the 64-VGPR row kernels
     __builtin_amdgcn_sched_barrier(0);
   }
+}
+
+// Radix-32 FIRST stage on lane pairs (MODE 3; L = 1), decimation in frequency.  Lane e of
+// butterfly i loads x_r, r = 16 e + r' (r' < 16), from x[i + r N/32].  One v_permlane32_swap per
+// dword pairs (x_r, x_{r+16}) for even r in the low half-wave and odd r in the high half; each
+// lane forms y_r = x_r + x_{r+16} and z_r = (x_r - x_{r+16}) w32^r; a second swap gathers every
+// y in the low half and every z in the high half, and one DFT16 per lane gives
+// v[k] = X_{2k+e} (X_{2k} = DFT16(y)_k, X_{2k+1} = DFT16(z)_k).  No input twiddles (L = 1).
+template <bool INV, int N, class In>
+__device__ __forceinline__ void stage_r32_pair_first(int tid, In& in, float2 (&v)[16]) {
+  constexpr int LP = N / 32;
+  // w32^{2p} = exp(-2 pi i p / 16), p < 8
+  constexpr float C16C[8] = {1.0f, 0.92387953251128675613f, 0.70710678118654752440f, 0.38268343236508977173f,
+                             0.0f, -0.38268343236508977173f, -0.70710678118654752440f, -0.92387953251128675613f};
+  constexpr float C16S[8] = {0.0f, 0.38268343236508977173f, 0.70710678118654752440f, 0.92387953251128675613f,
+                             1.0f, 0.92387953251128675613f, 0.70710678118654752440f, 0.38268343236508977173f};
+  const int e = (tid >> 5) & 1, i = pair_i(tid);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = in(0, r, i + (16 * e + r) * LP);
+  // w32^e
+  const float2 f1 = e ? make_float2(0.98078528040323044913f, -0.19509032201612826785f) : make_float2(1.f, 0.f);
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    float2 a = v[2 * p], b = v[2 * p + 1];
+    swap_halves(a.x, b.x);
+    swap_halves(a.y, b.y);
+    // (a, b) = (x_r, x_{r+16}), r = 2p + e;  w32^r = w32^{2p} w32^e
+    const float2 y = cadd(a, b);
+    const float2 z = cmul_tw<INV>(csub(a, b), p == 0 ? f1 : cmul(f1, make_float2(C16C[p], -C16S[p])));
+    float2 lo = y, hi = z;
+    swap_halves(lo.x, hi.x);
+    swap_halves(lo.y, hi.y);
+    v[2 * p] = lo;      // low half: y_{2p}, high half: z_{2p}
+    v[2 * p + 1] = hi;  // low half: y_{2p+1}, high half: z_{2p+1}
+  }
+  dftR<16, INV>(v);
 }
 
 // The pair stage reads x[i + (2s+e) L] at base lay(i + e L) plus lay(2 s L) - lay(0): true for
@@ -723,6 +764,37 @@ template <bool INV, int N, int T, int MODE, int S = 0, int L = 1, class Tw, clas
 __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int tid, In& in, Sv& sv) {
   using P = Pow2Sched<N>;
   constexpr int R = P::radix(S, MODE);
+  if constexpr (R == 32 && S == 0) {
+    // lane-pair radix-32 first stage (MODE 3), then the exchange into the L = 32 stage: lane
+    // (i, e) holds X_{2k+e}, Stockham output j = 32 i + 2k + e (conflict-free on split_lay<1>:
+    // 32 consecutive i per lane group)
+    static_assert(T == N / 16 && P::radix(1, MODE) == 16 && P::nst(MODE) >= 2, "pair-first layout");
+    constexpr int NB2 = N / 16;
+    constexpr int MB2 = NB2 / T;
+    float2 v1[16];
+    stage_r32_pair_first<INV, N>(tid, in, v1);
+    float2 nx[MB2][16];
+    float* dst = lds + split_lay<1>(32 * pair_i(tid) + ((tid >> 5) & 1));
+#pragma unroll
+    for (int part = 0; part < 2; ++part) {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 16; ++k) dst[split_lay<1>(2 * k) - split_lay<1>(0)] = part ? v1[k].y : v1[k].x;
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < MB2; ++m) {
+        const float* src = lds + split_lay<1>(tid + m * T);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float x = src[split_lay<1>(m * T + r * NB2) - split_lay<1>(m * T)];
+          if (part) nx[m][r].y = x;
+          else nx[m][r].x = x;
+        }
+      }
+    }
+    auto in2 = [&](int m, int r, int) { return nx[m][r]; };
+    fft_pow2_split_io<INV, N, T, MODE, 1, 32>(lds, tw, tid, in2, sv);
+  } else {
   constexpr int MB = N / R / T;
   float2 v[MB][R];
   stage_core<R, INV, N, L, T>(tw, tid, in, v);
@@ -787,6 +859,7 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
       auto in2 = [&](int m, int r, int) { return nx[m][r]; };
       fft_pow2_split_io<INV, N, T, MODE, S + 1, L * R>(lds, tw, tid, in2, sv);
     }
+  }
   }
 }
 
