@@ -32,6 +32,7 @@ constexpr float BASE_PLANE = 2e-3f;  // BASE_PLANE_THICKNESS (:23)
 
 struct ModArgs {
   int B, C, H, W, hs, ws;
+  int bl;  // batch lanes per block of the backward (power of two <= 16)
   int has_noise;
   float tol, eps, tand;
   float lam[THZ_MAX_WAVELENGTHS];
@@ -67,6 +68,7 @@ __device__ __forceinline__ float2 transmission(float hv, float lam, const ModArg
   return make_float2(loss * cs, loss * sn);
 }
 
+// grid (pixel blocks, batch stride): t_c(h) once per pixel, thread and wavelength
 __global__ void doe_modulate_fwd(const float2* __restrict__ f, const float* __restrict__ h,
                                  const float* __restrict__ u, float2* __restrict__ out, float* __restrict__ hfull,
                                  ModArgs a) {
@@ -76,48 +78,69 @@ __global__ void doe_modulate_fwd(const float2* __restrict__ f, const float* __re
   const int y = p / a.W, x = p - y * a.W;
   const int src = nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W);
   const float hv = noisy_h(h, u, src, a);
-  if (hfull) hfull[p] = hv;
+  if (hfull && blockIdx.y == 0) hfull[p] = hv;
   for (int c = 0; c < a.C; ++c) {
     const float2 t = transmission(hv, a.lam[c], a, nullptr);
-    for (int b = 0; b < a.B; ++b) {
+    for (int b = blockIdx.y; b < a.B; b += gridDim.y) {
       const size_t i = ((size_t)b * a.C + c) * HW + p;
       out[i] = cmul(f[i], t);
     }
   }
 }
 
-__global__ void doe_modulate_bwd(const float2* __restrict__ g, const float2* __restrict__ f,
-                                 const float* __restrict__ h, const float* __restrict__ u,
-                                 float2* __restrict__ gf, float* __restrict__ gh, ModArgs a) {
+// Block = MOD_THREADS threads = (MOD_THREADS / a.bl) pixels x a.bl batch lanes (a.bl a power of two
+// <= 16 chosen from B): consecutive threads take consecutive pixels, batch lane l walks
+// b = l, l + bl, ...; the height gradient's batch sum is finished across the lanes in LDS in a
+// fixed order (deterministic, no atomics for same-size maps).
+constexpr int MOD_THREADS = 256;
+
+__global__ void __launch_bounds__(MOD_THREADS) doe_modulate_bwd(const float2* __restrict__ g,
+                                                                const float2* __restrict__ f,
+                                                                const float* __restrict__ h,
+                                                                const float* __restrict__ u,
+                                                                float2* __restrict__ gf, float* __restrict__ gh,
+                                                                ModArgs a) {
+  __shared__ float red[MOD_THREADS];
   const int HW = a.H * a.W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= HW) return;
-  const int y = p / a.W, x = p - y * a.W;
-  const int src = nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W);
-  const float hv = noisy_h(h, u, src, a);
+  const int PX = MOD_THREADS / a.bl;
+  const int px = threadIdx.x % PX, lane = threadIdx.x / PX;
+  const int p = blockIdx.x * PX + px;
+  const bool live = p < HW;
   float acc = 0.f;
-  for (int c = 0; c < a.C; ++c) {
-    float2 gam;
-    const float2 t = transmission(hv, a.lam[c], a, &gam);
-    float2 gt = make_float2(0.f, 0.f);  // sum_b g conj(f)
-    for (int b = 0; b < a.B; ++b) {
-      const size_t i = ((size_t)b * a.C + c) * HW + p;
-      const float2 gv = g[i];
-      if (gf) gf[i] = make_float2(gv.x * t.x + gv.y * t.y, gv.y * t.x - gv.x * t.y);
-      if (gh) {
-        const float2 fv = f[i];
-        gt.x += gv.x * fv.x + gv.y * fv.y;
-        gt.y += gv.y * fv.x - gv.x * fv.y;
+  int src = 0;
+  if (live) {
+    const int y = p / a.W, x = p - y * a.W;
+    src = nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W);
+    const float hv = noisy_h(h, u, src, a);
+    for (int c = 0; c < a.C; ++c) {
+      float2 gam;
+      const float2 t = transmission(hv, a.lam[c], a, &gam);
+      float2 gt = make_float2(0.f, 0.f);  // sum_b g conj(f), this lane's share
+      for (int b = lane; b < a.B; b += a.bl) {
+        const size_t i = ((size_t)b * a.C + c) * HW + p;
+        const float2 gv = g[i];
+        if (gf) gf[i] = make_float2(gv.x * t.x + gv.y * t.y, gv.y * t.x - gv.x * t.y);
+        if (gh) {
+          const float2 fv = f[i];
+          gt.x += gv.x * fv.x + gv.y * fv.y;
+          gt.y += gv.y * fv.x - gv.x * fv.y;
+        }
       }
-    }
-    if (gh) {
-      const float2 dt = cmul(t, gam);  // dt/dh
-      acc += gt.x * dt.x + gt.y * dt.y;  // Re(gt conj(dt))
+      if (gh) {
+        const float2 dt = cmul(t, gam);  // dt/dh
+        acc += gt.x * dt.x + gt.y * dt.y;  // Re(gt conj(dt))
+      }
     }
   }
   if (gh) {
-    if (a.hs == a.H && a.ws == a.W) gh[src] = acc;
-    else atomicAdd(gh + src, acc);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (live && lane == 0) {
+      float s = red[px];
+      for (int l = 1; l < a.bl; ++l) s += red[l * PX + px];
+      if (a.hs == a.H && a.ws == a.W) gh[src] = s;
+      else atomicAdd(gh + src, s);
+    }
   }
 }
 
@@ -393,8 +416,8 @@ extern "C" int thz_doe_modulate_forward(const thz_doe_desc* d, const void* field
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("doe_modulate_fwd", s);
   const int n = d->H * d->W;
-  hipLaunchKernelGGL(doe_modulate_fwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)field, height, noise,
-                     (float2*)out, height_full, a);
+  hipLaunchKernelGGL(doe_modulate_fwd, dim3((n + 255) / 256, std::min(d->B, 64)), dim3(256), 0, s,
+                     (const float2*)field, height, noise, (float2*)out, height_full, a);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;
@@ -415,7 +438,10 @@ extern "C" int thz_doe_modulate_backward(const thz_doe_desc* d, const void* grad
   if (grad_height && (d->hs != d->H || d->ws != d->W))
     THZ_HIP_CHECK(hipMemsetAsync(grad_height, 0, sizeof(float) * d->hs * d->ws, s));
   const int n = d->H * d->W;
-  hipLaunchKernelGGL(doe_modulate_bwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)grad_out,
+  a.bl = 1;
+  while (a.bl < 16 && 2 * a.bl <= d->B) a.bl *= 2;
+  const int px = MOD_THREADS / a.bl;
+  hipLaunchKernelGGL(doe_modulate_bwd, dim3((n + px - 1) / px), dim3(MOD_THREADS), 0, s, (const float2*)grad_out,
                      (const float2*)field, height, noise, (float2*)grad_field, grad_height, a);
   THZ_LAUNCH_CHECK();
   kt.stop();

@@ -10,6 +10,7 @@
 //                      (experiment_four_focal_spots.ipynb:336-370): one workgroup per batch item
 //                      finds max / argmax of |E|^2, the squared error and the sum the backward's
 //                      max-path needs; the backward is then one elementwise pass.
+#include <algorithm>
 #include <cmath>
 
 #include "thz_common.hpp"
@@ -92,14 +93,16 @@ __device__ __forceinline__ bool aperture_open(const ApertureArgs& a, int i, int 
   return sqrtf(X * X + Y * Y) <= a.radius;
 }
 
+// grid (pixel blocks, planes): the mask is evaluated once per pixel and plane stride
 __global__ void aperture_kernel(const float2* __restrict__ in, float2* __restrict__ out, ApertureArgs a) {
   const int HW = a.H * a.W;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= HW) return;
   const bool open = aperture_open(a, p / a.W, p % a.W);
-  for (int bc = 0; bc < a.BC; ++bc) {
+  for (int bc = blockIdx.y; bc < a.BC; bc += gridDim.y) {
     const size_t idx = (size_t)bc * HW + p;
-    out[idx] = open ? in[idx] : make_float2(0.f * in[idx].x, 0.f * in[idx].y);
+    const float2 v = in[idx];
+    out[idx] = open ? v : make_float2(0.f * v.x, 0.f * v.y);
   }
 }
 
@@ -408,7 +411,8 @@ extern "C" int thz_aperture(const thz_aperture_desc* d, const void* in, void* ou
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("aperture", s);
   const int n = d->H * d->W;
-  hipLaunchKernelGGL(aperture_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out, a);
+  hipLaunchKernelGGL(aperture_kernel, dim3((n + 255) / 256, std::min(a.BC, 64)), dim3(256), 0, s, (const float2*)in,
+                     (float2*)out, a);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;
