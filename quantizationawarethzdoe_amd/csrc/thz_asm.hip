@@ -360,6 +360,124 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
   }
 }
 
+// K2 for a compile-time mixed-radix Ph (MxPlan, blockDim MX_T): the power-of-two kernel's
+// structure -- spectrum kept in registers, H_z applied in the inverse's loader from the
+// per-column sqrt and the bisected |m_x| bound, cropped rows stored from the last stage -- with
+// the runtime plan's numerics at the output (1 / (Ph Pw) is not a power of two here, so the
+// scale is applied to each output element as asm_cols<0> does).
+constexpr int MX_T = 64;
+#ifndef THZ_MX_WPE
+#define THZ_MX_WPE 8
+#endif
+#ifndef MX_PAR_Z
+#define MX_PAR_Z 2  // z-chunks up to this size find their row bounds lane-parallel
+#endif
+template <class MP>
+__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_MX_WPE))) asm_cols_mx(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                    AsmArgs a) {
+  constexpr int PN = MP::N, RL = MP::RL, NBL = PN / RL, MBL = (NBL + MX_T - 1) / MX_T;
+  static_assert(MP::R0 == RL, "the inverse must start where the forward ends");
+  extern __shared__ float2 lds[];
+  int id, z_lo = 0, z_hi = a.nz;
+  if ((int)blockIdx.x < a.kfull) {
+    id = xcd_chunk(blockIdx.x, a.kfull);
+  } else {
+    const int t = blockIdx.x - a.kfull, part = t % a.kparts;
+    id = a.kfull + t / a.kparts;
+    z_lo = part * a.nz / a.kparts;
+    z_hi = (part + 1) * a.nz / a.kparts;
+  }
+  const int bc = id / a.ncols, c = id - bc * a.ncols;
+  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
+  const float lam = a.lam[bc % a.C];
+  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
+  int tid = threadIdx.x;
+  float2 sp[MBL][RL];
+  auto ld0 = [&](int, int, int idx) {
+    const int s = idx - a.in_r0;
+    return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
+  };
+  auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
+  const auto twr = MP::template twiddles<MX_T>(ph.tw, tid);
+  MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
+  if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
+    const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
+    int tz = threadIdx.x;
+    asm volatile("" : "+v"(tz));
+    auto ld1 = [&](int m, int r, int idx) {
+      const float2 t = tcol[idx];
+      return cmul(sp[m][r], a.adjoint ? make_float2(t.x, -t.y) : t);
+    };
+    float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+    auto sv1 = [&](int, int, int j, float2 v) {
+      const int r = j - a.out_r0;
+      if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+    };
+    MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
+    return;
+  }
+  // kept rows of this column per z: |m_x| <= M_z (see asm_cols)
+  int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN));
+  const float kl = TWO_PI_F / lam;
+  const float kl2 = tf_mul(kl, kl);
+  const float Ky2 = tf_mul(Ky, Ky);
+  if (z_hi - z_lo <= MX_PAR_Z) {
+    // few planes (the DONN / QAT layers: one): every lane tests ceil((PN/2+1)/64) rows of each
+    // plane and M_z + 1 is the number that pass (the kept set is a prefix of |m_x|) -- a
+    // one-lane bisection would cost the whole wave its ~9 serial rounds of fp32 divisions
+    for (int zz = z_lo; zz < z_hi; ++zz) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      int n = 0;
+#pragma unroll
+      for (int m0 = 0; m0 <= PN / 2; m0 += MX_T) {
+        const int m = m0 + (int)threadIdx.x;
+        n += __popcll(__ballot(m <= PN / 2 && tf_pass(a.bl, PN, a.dx, s, Ky, m)));
+      }
+      if (threadIdx.x == 0) mz[zz - z_lo] = n - 1;
+    }
+  } else if ((int)threadIdx.x < z_hi - z_lo) {
+    const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + threadIdx.x]);
+    int lo = -1, hi = PN / 2 + 1;
+    if (tf_pass(a.bl, PN, a.dx, s, Ky, 0)) {
+      lo = 0;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tf_pass(a.bl, PN, a.dx, s, Ky, mid)) lo = mid;
+        else hi = mid;
+      }
+    }
+    mz[threadIdx.x] = lo;
+  }
+  float sq[MBL][RL];
+#pragma unroll
+  for (int m = 0; m < MBL; ++m)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) {
+      const float Kx = kfreq(freq_index(tid + m * MX_T + r * NBL, PN), PN, a.dx);
+      sq[m][r] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
+    }
+  __syncthreads();  // mz visible
+  for (int zz = z_lo; zz < z_hi; ++zz) {
+    const float z = a.zv[a.zoff + zz];
+    const int M = mz[zz - z_lo];
+    int tz = threadIdx.x;
+    asm volatile("" : "+v"(tz));
+    auto ld1 = [&](int m, int r, int idx) {
+      const int mx = freq_index(idx, PN);
+      if (mx > M || -mx > M) return make_float2(0.f, 0.f);
+      float sn, cs;
+      sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
+      return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
+    };
+    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+    auto sv1 = [&](int, int, int j, float2 v) {
+      const int r = j - a.out_r0;
+      if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+    };
+    MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // K3: per output row: gather band from U, IFFT(Pw), crop -> out[z][bc][r][w]
 // ---------------------------------------------------------------------------------------------
@@ -650,6 +768,12 @@ static int ensure_lds_attr() {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Workgroups of the column pass resident on the whole device at once (CUs x occupancy).
+#ifndef THZ_MX
+#define THZ_MX 1
+#endif
+// Ph with a compile-time mixed-radix column kernel (asm_cols_mx), else 0
+static int mx_kind(int n) { return THZ_MX && n == Mx300::N ? n : 0; }
+
 static int k2_resident(int Ph, int threads, size_t lds) {
   static std::mutex mu;
   static std::map<std::pair<int, int>, int> cache;
@@ -668,6 +792,7 @@ static int k2_resident(int Ph, int threads, size_t lds) {
     case 16384: k = (const void*)asm_cols<16384>; break;
     default: k = (const void*)asm_cols<0>; break;
   }
+  if (mx_kind(Ph) == Mx300::N) k = (const void*)asm_cols_mx<Mx300>;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -715,9 +840,15 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     a.nz = std::min(g.zc, Z - z0);
     {
       KernelTimer kt("asm_cols", s);
-      const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-      const int ntask = k2_tasks(g, &a, th, lds2);
-      THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
+      if (mx_kind(g.Ph) == Mx300::N) {
+        const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
+        const int ntask = k2_tasks(g, &a, MX_T, lds2);
+        hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+      } else {
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        const int ntask = k2_tasks(g, &a, th, lds2);
+        THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
+      }
       THZ_LAUNCH_CHECK();
       kt.stop();
     }

@@ -885,6 +885,126 @@ __device__ __forceinline__ void fft_pow2(float2* lds, const Tw& tw, int tid) {
   fft_pow2_io<INV, N, T, false, true, true>(lds, tw, tid, io, io);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Compile-time mixed-radix plans (non-power-of-two sizes with a fixed radix list, e.g.
+// 300 = 5·3·4·5): the runtime plan's Stockham stages with N, L, R and the thread count known to
+// the compiler (constant-divisor index math, exact butterfly trip counts, inlined), and the
+// same fused I/O contract as fft_pow2_io: the first stage reads operand i + r N/R0 through
+// ld(m, r, idx), the last stage hands result i + r N/Rlast to sv(m, r, j) from registers, with
+// butterfly i = tid + m T.  A transform whose first radix equals the previous one's last radix
+// therefore reads exactly the elements the previous transform left in this thread's registers.
+// Twiddles exp(-+2 pi i k t / N) come from the plan's global table (L2-resident, N float2).
+// ---------------------------------------------------------------------------------------------
+#ifndef THZ_MX_TWR
+#define THZ_MX_TWR 1  // stage twiddles held in registers (1) or read from the table per stage (0)
+#endif
+template <bool INV, int N, int T, int L, int R, bool FIRST, bool LAST, int MW, class Ld, class Sv>
+__device__ __forceinline__ void mx_stage(float2* lds, const float2 (&w1)[MW], const float2* __restrict__ tw, int tid,
+                                         Ld& ld, Sv& sv) {
+  constexpr int NB = N / R;
+  constexpr int MB = (NB + T - 1) / T;
+  static_assert(MB <= MW, "mixed plan: twiddle registers");
+  float2 v[MB][R];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int i = tid + m * T;
+    if (NB % T == 0 || i < NB) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (FIRST) v[m][r] = ld(m, r, i + r * NB);
+        else v[m][r] = lds[padx(i + r * NB)];
+      }
+      if constexpr (L > 1) {
+        const float2 w = THZ_MX_TWR ? w1[m] : tw[(i % L) * (N / (L * R))];
+        float2 wr = w;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          v[m][r] = cmul_tw<INV>(v[m][r], wr);
+          if (r + 1 < R) wr = cmul(wr, w);
+        }
+      }
+      dftR<R, INV>(v[m]);
+    }
+  }
+  if constexpr (LAST) {
+    static_assert(L * R == N, "mixed plan: radices must multiply to N");
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int i = tid + m * T;
+      if (NB % T == 0 || i < NB) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) sv(m, r, i + r * NB, v[m][r]);
+      }
+    }
+  } else {
+    __syncthreads();  // every read of this stage (or the previous transform's) is done
+#pragma unroll
+    for (int m = 0; m < MB; ++m) {
+      const int i = tid + m * T;
+      if (NB % T == 0 || i < NB) {
+        const int k = i % L;
+        const int j = (i - k) * R + k;
+#pragma unroll
+        for (int r = 0; r < R; ++r) lds[padx(j + r * L)] = v[m][r];
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <bool INV, int N, int T, int L, int S, bool FIRST, int NS, int MW, class Ld, class Sv, int R, int... Rest>
+__device__ __forceinline__ void mx_stages(float2* lds, const float2 (&w1)[NS][MW], const float2* __restrict__ tw, int tid,
+                                          Ld& ld, Sv& sv) {
+  mx_stage<INV, N, T, L, R, FIRST, sizeof...(Rest) == 0>(lds, w1[S], tw, tid, ld, sv);
+  if constexpr (sizeof...(Rest) > 0)
+    mx_stages<INV, N, T, L * R, S + 1, false, NS, MW, Ld, Sv, Rest...>(lds, w1, tw, tid, ld, sv);
+}
+
+// The per-thread stage twiddles exp(-2 pi i k / (L R)), k = i mod L, of every stage, loaded once
+// from the plan's table (tw[k N / (L R)]) and kept in registers across transforms.
+template <int N, int T, int... Rs>
+struct MxTw {
+  static constexpr int NS = sizeof...(Rs);
+  static constexpr int MW = (N / 2 + T - 1) / T;  // butterflies per thread of the smallest radix
+  float2 w[NS][MW];
+  const float2* tw;
+  template <int L, int S, int R, int... Rest>
+  __device__ __forceinline__ void fill(const float2* __restrict__ tw, int tid) {
+    if (!THZ_MX_TWR) return;
+    constexpr int NB = N / R, MB = (NB + T - 1) / T;
+#pragma unroll
+    for (int m = 0; m < MW; ++m) {
+      const int i = tid + m * T;
+      w[S][m] = (L > 1 && m < MB && i < NB) ? tw[(i % L) * (N / (L * R))] : make_float2(1.f, 0.f);
+    }
+    if constexpr (sizeof...(Rest) > 0) fill<L * R, S + 1, Rest...>(tw, tid);
+  }
+};
+
+template <int... Rs>
+struct MxPlan {
+  static constexpr int N = (Rs * ...);
+  static constexpr int RADIX[] = {Rs...};
+  static constexpr int R0 = RADIX[0];
+  static constexpr int RL = RADIX[sizeof...(Rs) - 1];
+  template <int T>
+  using Tw = MxTw<N, T, Rs...>;
+  template <int T>
+  __device__ __forceinline__ static Tw<T> twiddles(const float2* __restrict__ tw, int tid) {
+    Tw<T> t;
+    t.tw = tw;
+    t.template fill<1, 0, Rs...>(tw, tid);
+    return t;
+  }
+  template <bool INV, int T, class Ld, class Sv>
+  __device__ __forceinline__ static void run(float2* lds, const Tw<T>& t, int tid, Ld& ld, Sv& sv) {
+    mx_stages<INV, N, T, 1, 0, true, Tw<T>::NS, Tw<T>::MW, Ld, Sv, Rs...>(lds, t.w, t.tw, tid, ld, sv);
+  }
+};
+// 300 = 5 3 4 5: first and last radix 5 (60 butterflies: one per lane of a 64-thread workgroup),
+// so the forward's spectrum is 5 values per lane and the inverse starts from it directly
+using Mx300 = MxPlan<5, 3, 4, 5>;
+
 // Full transform of one row held in LDS (natural order in and out).  Unnormalised.
 template <bool INV>
 __device__ void fft_lds(float2* lds, const FftPlan& p, int tid, int nthr) {
