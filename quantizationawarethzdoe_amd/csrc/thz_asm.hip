@@ -137,6 +137,20 @@ struct Geo {
   static constexpr int T = PN > 0 ? PN / pow2_v(PN) : 0;
 };
 
+// Compile-time mixed-radix sizes (MxPlan, one 64-thread workgroup per transform): the P = 300
+// grid of the cfg4 / cfg5 layers.  Other non-power-of-two sizes run the runtime plan.
+constexpr int MX_T = 64;
+#ifndef THZ_MX
+#define THZ_MX 1
+#endif
+#ifndef THZ_MX_WPE
+#define THZ_MX_WPE 8
+#endif
+#ifndef MX_PAR_Z
+#define MX_PAR_Z 2  // z-chunks up to this size find their row bounds lane-parallel
+#endif
+__host__ __device__ constexpr bool is_mx(int n) { return THZ_MX && n == Mx300::N; }
+
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
   const int c = freq_index(j, P) + J;
   return (c >= 0 && c < ncols) ? c : -1;
@@ -171,7 +185,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
     if (!ez) return src[s];
     return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
   };
-  if constexpr (PN > 0) {
+  if constexpr (PN > 0 && !is_mx(PN)) {
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     auto ld = [&](int, int, int idx) {
       const int s = idx - a.in_c0;
@@ -182,6 +196,17 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
     fft_pow2_run<false, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
+  } else if constexpr (is_mx(PN)) {
+    const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
+    auto ld = [&](int, int, int idx) {
+      const int s = idx - a.in_c0;
+      return (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
+    };
+    auto sv = [&](int, int, int j, float2 v) {
+      const int c = band_col(j, PN, a.J, a.ncols);
+      if (c >= 0) dst[blk(c, h, a.Hin)] = v;
+    };
+    Mx300::run<false, MX_T>(lds, twr, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
@@ -365,13 +390,6 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
 // per-column sqrt and the bisected |m_x| bound, cropped rows stored from the last stage -- with
 // the runtime plan's numerics at the output (1 / (Ph Pw) is not a power of two here, so the
 // scale is applied to each output element as asm_cols<0> does).
-constexpr int MX_T = 64;
-#ifndef THZ_MX_WPE
-#define THZ_MX_WPE 8
-#endif
-#ifndef MX_PAR_Z
-#define MX_PAR_Z 2  // z-chunks up to this size find their row bounds lane-parallel
-#endif
 template <class MP>
 __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_MX_WPE))) asm_cols_mx(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                     AsmArgs a) {
@@ -490,7 +508,18 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
   const int tid = threadIdx.x, nt = blockDim.x;
   const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
-  if constexpr (PN > 0) {
+  if constexpr (is_mx(PN)) {
+    const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
+    auto ld = [&](int, int, int j) {
+      const int c = band_col(j, PN, a.J, a.ncols);
+      return c >= 0 ? src[blk_u(c, r, a.Hout)] : make_float2(0.f, 0.f);
+    };
+    auto sv = [&](int, int, int j, float2 v) {
+      const int w = j - a.out_c0;
+      if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
+    };
+    Mx300::run<true, MX_T>(lds, twr, tid, ld, sv);
+  } else if constexpr (PN > 0) {
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
     // First stage (radix 16, L = 1) reads j = i + q*NB0, i < NB0.  Its band column is
     // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
@@ -768,11 +797,12 @@ static int ensure_lds_attr() {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Workgroups of the column pass resident on the whole device at once (CUs x occupancy).
-#ifndef THZ_MX
-#define THZ_MX 1
-#endif
-// Ph with a compile-time mixed-radix column kernel (asm_cols_mx), else 0
-static int mx_kind(int n) { return THZ_MX && n == Mx300::N ? n : 0; }
+// Ph / Pw with a compile-time mixed-radix kernel (asm_cols_mx, asm_rows_*<N>), else 0
+static int mx_kind(int n) { return is_mx(n) ? n : 0; }
+// K1 / K3: the mixed-radix instantiation or the power-of-two switch
+#define THZ_ROWS_SWITCH(n, KER, G, LDSB, ...)                                                      \
+  if (mx_kind(n) == Mx300::N) hipLaunchKernelGGL(KER<Mx300::N>, G, dim3(MX_T), LDSB, __VA_ARGS__); \
+  else THZ_POW2_SWITCH(n, KER, G, dim3(threads_for(n)), LDSB, __VA_ARGS__)
 
 static int k2_resident(int Ph, int threads, size_t lds) {
   static std::mutex mu;
@@ -827,11 +857,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
                         hipStream_t s, FftPlan pw, FftPlan ph) {
   int e;
   if ((e = ensure_lds_attr())) return e;
-  const int tw = threads_for(g.Pw), th = threads_for(g.Ph);
+  const int th = threads_for(g.Ph);
   {
     KernelTimer kt("asm_rows_fwd", s);
-    THZ_POW2_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), dim3(tw), fft_lds_bytes_io(g.Pw), s, (const float2*)in,
-                    T, pw, a);
+    THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in, T, pw, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
@@ -854,8 +883,8 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     }
     {
       KernelTimer kt("asm_rows_inv", s);
-      THZ_POW2_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), dim3(tw), fft_lds_bytes_io(g.Pw), s,
-                      (const float2*)U, (float2*)out, pw, a);
+      THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
+                      (float2*)out, pw, a);
       THZ_LAUNCH_CHECK();
       kt.stop();
     }
