@@ -48,6 +48,8 @@ struct AsmArgs {
   const float2* tft;  // RSC: column-major transfer-function table [C][ncols][Ph] (nullptr: analytic ASM)
   int vec;            // VRS: plane b == 2 is Ez = (Ex x + Ey y) / r computed in the row pass
   float zr;           // VRS: z of the Ez grid
+  float* sqt;         // mixed-radix K2: sqrt(k^2 - Kx^2 - Ky^2) per [C][ncols][Ph] (asm_tf_tables)
+  int* mzt;           // mixed-radix K2: kept-row bound M_z per [C][ncols][nz] of the current z-chunk
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
@@ -145,9 +147,6 @@ constexpr int MX_T = 64;
 #endif
 #ifndef THZ_MX_WPE
 #define THZ_MX_WPE 8
-#endif
-#ifndef MX_PAR_Z
-#define MX_PAR_Z 2  // z-chunks up to this size find their row bounds lane-parallel
 #endif
 __host__ __device__ constexpr bool is_mx(int n) { return THZ_MX && n == Mx300::N; }
 
@@ -385,6 +384,40 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
   }
 }
 
+// Per (wavelength, band column) of a mixed-radix Ph: sqrt(k^2 - Kx^2 - Ky^2) of every row
+// (z-independent, written on the first z-chunk) and the kept-row bound M_z of each z of the
+// chunk (bisection with the exact reference-order tests, one lane per z; see asm_cols).  Every
+// plane of the wavelength shares them, so the column pass does no fp32 division.
+template <int PN>
+__global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
+  const int li = blockIdx.x / a.ncols, c = blockIdx.x - li * a.ncols;
+  const float lam = a.lam[li];
+  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
+  const size_t col = (size_t)li * a.ncols + c;
+  if (with_sq) {
+    const float kl = TWO_PI_F / lam;
+    const float kl2 = tf_mul(kl, kl);
+    const float Ky2 = tf_mul(Ky, Ky);
+    for (int i = threadIdx.x; i < PN; i += blockDim.x) {
+      const float Kx = kfreq(freq_index(i, PN), PN, a.dx);
+      a.sqt[col * PN + i] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
+    }
+  }
+  for (int zz = threadIdx.x; zz < a.nz; zz += blockDim.x) {
+    const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+    int lo = -1, hi = PN / 2 + 1;
+    if (tf_pass(a.bl, PN, a.dx, s, Ky, 0)) {
+      lo = 0;
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tf_pass(a.bl, PN, a.dx, s, Ky, mid)) lo = mid;
+        else hi = mid;
+      }
+    }
+    a.mzt[col * a.nz + zz] = lo;
+  }
+}
+
 // K2 for a compile-time mixed-radix Ph (MxPlan, blockDim MX_T): the power-of-two kernel's
 // structure -- spectrum kept in registers, H_z applied in the inverse's loader from the
 // per-column sqrt and the bisected |m_x| bound, cropped rows stored from the last stage -- with
@@ -407,8 +440,6 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_M
   }
   const int bc = id / a.ncols, c = id - bc * a.ncols;
   const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
-  const float lam = a.lam[bc % a.C];
-  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
   int tid = threadIdx.x;
   float2 sp[MBL][RL];
   auto ld0 = [&](int, int, int idx) {
@@ -434,50 +465,21 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_M
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
     return;
   }
-  // kept rows of this column per z: |m_x| <= M_z (see asm_cols)
-  int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN));
-  const float kl = TWO_PI_F / lam;
-  const float kl2 = tf_mul(kl, kl);
-  const float Ky2 = tf_mul(Ky, Ky);
-  if (z_hi - z_lo <= MX_PAR_Z) {
-    // few planes (the DONN / QAT layers: one): every lane tests ceil((PN/2+1)/64) rows of each
-    // plane and M_z + 1 is the number that pass (the kept set is a prefix of |m_x|) -- a
-    // one-lane bisection would cost the whole wave its ~9 serial rounds of fp32 divisions
-    for (int zz = z_lo; zz < z_hi; ++zz) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
-      int n = 0;
-#pragma unroll
-      for (int m0 = 0; m0 <= PN / 2; m0 += MX_T) {
-        const int m = m0 + (int)threadIdx.x;
-        n += __popcll(__ballot(m <= PN / 2 && tf_pass(a.bl, PN, a.dx, s, Ky, m)));
-      }
-      if (threadIdx.x == 0) mz[zz - z_lo] = n - 1;
-    }
-  } else if ((int)threadIdx.x < z_hi - z_lo) {
-    const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + threadIdx.x]);
-    int lo = -1, hi = PN / 2 + 1;
-    if (tf_pass(a.bl, PN, a.dx, s, Ky, 0)) {
-      lo = 0;
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (tf_pass(a.bl, PN, a.dx, s, Ky, mid)) lo = mid;
-        else hi = mid;
-      }
-    }
-    mz[threadIdx.x] = lo;
-  }
+  // kept rows |m_x| <= M_z per z and the z-independent sqrt(k^2 - K^2) of the elements this
+  // thread holds: the wavelength's per-column tables (asm_tf_tables)
+  const size_t tc = (size_t)(bc % a.C) * a.ncols + c;
+  const int* mzc = a.mzt + tc * a.nz;
+  const float* sqc = a.sqt + tc * PN;
   float sq[MBL][RL];
 #pragma unroll
-  for (int m = 0; m < MBL; ++m)
+  for (int m = 0; m < MBL; ++m) {
+    const int i = tid + m * MX_T;
 #pragma unroll
-    for (int r = 0; r < RL; ++r) {
-      const float Kx = kfreq(freq_index(tid + m * MX_T + r * NBL, PN), PN, a.dx);
-      sq[m][r] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
-    }
-  __syncthreads();  // mz visible
+    for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
+  }
   for (int zz = z_lo; zz < z_hi; ++zz) {
     const float z = a.zv[a.zoff + zz];
-    const int M = mz[zz - z_lo];
+    const int M = mzc[zz];
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
     auto ld1 = [&](int m, int r, int idx) {
@@ -660,6 +662,7 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
 // ---------------------------------------------------------------------------------------------
 struct AsmGeom {
   int BC, Ph, Pw, ncols, J, ncb, ncbu, Hin, Win, Hout, Wout, zc;
+  int C;
 };
 
 static int validate(const thz_asm_desc* d) {
@@ -713,6 +716,7 @@ static int band_half_width(const thz_asm_desc* d, int Ph, int Pw) {
 
 static void geometry(const thz_asm_desc* d, AsmGeom* g) {
   g->BC = d->B * d->C;
+  g->C = d->C;
   g->Ph = d->H + 2 * d->pad_h;
   g->Pw = d->W + 2 * d->pad_w;
   const int Ho = d->unpad ? d->H : g->Ph, Wo = d->unpad ? d->W : g->Pw;
@@ -847,17 +851,28 @@ static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds) {
   return full + rem * a->kparts;
 }
 
+// the mixed-radix column pass's per-(wavelength, column) tables, shared by every plane
+static size_t tab_sq_bytes(const AsmGeom& g) { return align256((size_t)g.C * g.ncols * g.Ph * sizeof(float)); }
+static size_t tab_bytes(const AsmGeom& g) {
+  return mx_kind(g.Ph) ? tab_sq_bytes(g) + align256((size_t)g.C * g.ncols * g.zc * sizeof(int)) : 0;
+}
 static size_t ws_bytes(const AsmGeom& g) {
   return align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)) +
-         align256((size_t)g.zc * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2));
+         align256((size_t)g.zc * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2)) + tab_bytes(g);
 }
 
 // K1 once, then (K2, K3) per z-chunk, on a prepared argument block.
 static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
-                        hipStream_t s, FftPlan pw, FftPlan ph) {
+                        hipStream_t s, FftPlan pw, FftPlan ph, char* tabs = nullptr) {
   int e;
   if ((e = ensure_lds_attr())) return e;
   const int th = threads_for(g.Ph);
+  const bool mx_tabs = mx_kind(g.Ph) == Mx300::N && !a.tft;
+  if (mx_tabs) {
+    if (!tabs) return fail(THZ_E_WORKSPACE, "mixed-radix column tables need workspace");
+    a.sqt = (float*)tabs;
+    a.mzt = (int*)(tabs + tab_sq_bytes(g));
+  }
   {
     KernelTimer kt("asm_rows_fwd", s);
     THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in, T, pw, a);
@@ -870,6 +885,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     {
       KernelTimer kt("asm_cols", s);
       if (mx_kind(g.Ph) == Mx300::N) {
+        if (mx_tabs) {
+          hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
+          THZ_LAUNCH_CHECK();
+        }
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
@@ -958,7 +977,8 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
 
   float2* T = (float2*)workspace;
   float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
-  return run_pipeline(a, g, d->Z, in, out, T, U, (hipStream_t)stream, pw, ph);
+  char* tabs = (char*)workspace + ws_bytes(g) - tab_bytes(g);
+  return run_pipeline(a, g, d->Z, in, out, T, U, (hipStream_t)stream, pw, ph, tab_bytes(g) ? tabs : nullptr);
 }
 
 extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream) {
