@@ -403,6 +403,22 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
       a.sqt[col * PN + i] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
     }
   }
+  if (a.nz <= 2) {
+    // few planes (the DONN / QAT layers: one): every lane tests ceil((PN/2+1)/64) rows and M_z + 1
+    // is the number that pass (the kept set is a prefix of |m_x|), instead of one lane's serial
+    // bisection
+    for (int zz = 0; zz < a.nz; ++zz) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      int n = 0;
+#pragma unroll
+      for (int m0 = 0; m0 <= PN / 2; m0 += MX_T) {
+        const int m = m0 + (int)threadIdx.x;
+        n += __popcll(__ballot(m <= PN / 2 && tf_pass(a.bl, PN, a.dx, s, Ky, m)));
+      }
+      if (threadIdx.x == 0) a.mzt[col * a.nz + zz] = n - 1;
+    }
+    return;
+  }
   for (int zz = threadIdx.x; zz < a.nz; zz += blockDim.x) {
     const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
     int lo = -1, hi = PN / 2 + 1;

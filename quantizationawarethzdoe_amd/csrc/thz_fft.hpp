@@ -1003,7 +1003,10 @@ struct MxPlan {
 };
 // 300 = 5 3 4 5: first and last radix 5 (60 butterflies: one per lane of a 64-thread workgroup),
 // so the forward's spectrum is 5 values per lane and the inverse starts from it directly
-using Mx300 = MxPlan<5, 3, 4, 5>;
+#ifndef THZ_MX_PLAN
+#define THZ_MX_PLAN 0
+#endif
+using Mx300 = std::conditional_t<THZ_MX_PLAN == 0, MxPlan<5, 3, 4, 5>, MxPlan<5, 4, 3, 5>>;
 
 // Full transform of one row held in LDS (natural order in and out).  Unnormalised.
 template <bool INV>
