@@ -72,7 +72,7 @@ def test_rsc_1024_vs_oracle():
     assert rel_l2(out, ref) <= 5e-4
 
 
-@pytest.mark.parametrize("H,W,C", [(40, 48, 2), (33, 50, 1)])
+@pytest.mark.parametrize("H,W,C", [(40, 48, 2), (33, 50, 1), (150, 150, 2)])  # 150: P = 300, the mixed-radix kernels
 def test_rsc_backward_vs_oracle_autograd(H, W, C):
     """RSC_prop backward (adjoint kernels) vs autograd through the fp64 oracle."""
     from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
