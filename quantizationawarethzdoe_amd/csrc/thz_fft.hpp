@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <utility>
 
 namespace thz {
 
@@ -272,6 +273,70 @@ __device__ __forceinline__ void dft7(float2* v) {
   v[4] = make_float2(m3.x + p3.y, m3.y - p3.x);
 }
 
+// Composite in-register DFT of N = R1 R2 points (natural order in and out), Cooley-Tukey:
+// R1 DFTs of R2 points over n2 of v[n1 + R1 n2], twiddles W_N^(n1 k2) folded to compile-time
+// constants, then R2 DFTs of R1 points -> v[k2 + R2 k1].
+constexpr double ce_pi = 3.14159265358979323846;
+constexpr double ce_sin_red(double x) {  // |x| <= pi
+  double t = x, s = x;
+  for (int k = 1; k < 14; ++k) {
+    t *= -x * x / ((2.0 * k) * (2.0 * k + 1.0));
+    s += t;
+  }
+  return s;
+}
+constexpr double ce_cos_red(double x) {
+  double t = 1.0, s = 1.0;
+  for (int k = 1; k < 14; ++k) {
+    t *= -x * x / ((2.0 * k - 1.0) * (2.0 * k));
+    s += t;
+  }
+  return s;
+}
+// exp(-2 pi i e / N) components, angle reduced to [-pi, pi]
+constexpr double ce_ang(int e, int n) {
+  const int r = e % n;
+  return 2.0 * ce_pi * (double)(2 * r > n ? r - n : r) / (double)n;
+}
+template <int N, int E>
+struct CeTw {
+  static constexpr float c = (float)ce_cos_red(ce_ang(E, N));
+  static constexpr float s = (float)-ce_sin_red(ce_ang(E, N));
+};
+
+template <int R, bool INV>
+__device__ __forceinline__ void dftR(float2* v);
+
+template <int R1, int R2, bool INV, int I>
+__device__ __forceinline__ void ct_tw_one(float2 (&t)[R1][R2]) {
+  constexpr int n1 = I / R2, k2 = I % R2, e = (n1 * k2) % (R1 * R2);
+  if constexpr (e != 0) t[n1][k2] = cmul_tw<INV>(t[n1][k2], make_float2(CeTw<R1 * R2, e>::c, CeTw<R1 * R2, e>::s));
+}
+template <int R1, int R2, bool INV, int... I>
+__device__ __forceinline__ void ct_tw_all(float2 (&t)[R1][R2], std::integer_sequence<int, I...>) {
+  (ct_tw_one<R1, R2, INV, I>(t), ...);
+}
+template <int R1, int R2, bool INV>
+__device__ __forceinline__ void dft_ct(float2* v) {
+  float2 t[R1][R2];
+#pragma unroll
+  for (int n1 = 0; n1 < R1; ++n1) {
+#pragma unroll
+    for (int n2 = 0; n2 < R2; ++n2) t[n1][n2] = v[n1 + R1 * n2];
+    dftR<R2, INV>(t[n1]);
+  }
+  ct_tw_all<R1, R2, INV>(t, std::make_integer_sequence<int, R1 * R2>{});
+#pragma unroll
+  for (int k2 = 0; k2 < R2; ++k2) {
+    float2 u[R1];
+#pragma unroll
+    for (int n1 = 0; n1 < R1; ++n1) u[n1] = t[n1][k2];
+    dftR<R1, INV>(u);
+#pragma unroll
+    for (int k1 = 0; k1 < R1; ++k1) v[k2 + R2 * k1] = u[k1];
+  }
+}
+
 template <int R, bool INV>
 __device__ __forceinline__ void dftR(float2* v) {
   if constexpr (R == 2) dft2<INV>(v[0], v[1]);
@@ -281,6 +346,9 @@ __device__ __forceinline__ void dftR(float2* v) {
   else if constexpr (R == 7) dft7<INV>(v);
   else if constexpr (R == 8) dft8<INV>(v);
   else if constexpr (R == 16) dft16<INV>(v);
+  else if constexpr (R == 15) dft_ct<3, 5, INV>(v);
+  else if constexpr (R == 20) dft_ct<4, 5, INV>(v);
+  else static_assert(R == 0, "no in-register DFT of this radix");
 }
 
 // ---------------------------------------------------------------------------------------------
