@@ -77,6 +77,10 @@ typedef struct thz_asm_desc {
   const float* z;           /* host [Z] */
 } thz_asm_desc;
 
+/* Workspace: the row-pass spectrum T [BC][ncols][H], one z-chunk of column-pass output
+ * U [zc][BC][ncols][Ho] (both complex64), and for a 300-point padded height the
+ * mixed-radix column pass's per-(wavelength, column) tables (sqrt row values and
+ * kept-row bounds).  Contents need not persist between calls. */
 int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes);
 int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
                     thz_stream_t stream);
