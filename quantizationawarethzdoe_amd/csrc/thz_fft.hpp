@@ -348,6 +348,7 @@ __device__ __forceinline__ void dftR(float2* v) {
   else if constexpr (R == 16) dft16<INV>(v);
   else if constexpr (R == 15) dft_ct<3, 5, INV>(v);
   else if constexpr (R == 20) dft_ct<4, 5, INV>(v);
+  else if constexpr (R == 12) dft_ct<4, 3, INV>(v);
   else static_assert(R == 0, "no in-register DFT of this radix");
 }
 
@@ -1074,7 +1075,8 @@ struct MxPlan {
 #ifndef THZ_MX_PLAN
 #define THZ_MX_PLAN 0
 #endif
-using Mx300 = std::conditional_t<THZ_MX_PLAN == 0, MxPlan<5, 3, 4, 5>, MxPlan<5, 4, 3, 5>>;
+using Mx300 = std::conditional_t<THZ_MX_PLAN == 0, MxPlan<5, 3, 4, 5>,
+                                 std::conditional_t<THZ_MX_PLAN == 1, MxPlan<5, 4, 3, 5>, MxPlan<5, 12, 5>>>;
 
 // Full transform of one row held in LDS (natural order in and out).  Unnormalised.
 template <bool INV>
