@@ -730,10 +730,10 @@ __global__ void __launch_bounds__(1024) rsc_k_cols(const float2* __restrict__ TK
 // ---------------------------------------------------------------------------------------------
 template <int PN>
 __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict__ in, float2* __restrict__ out,
-                                                       FftPlan p, int inverse) {
+                                                       FftPlan p, int inverse, size_t stride) {
   extern __shared__ float2 lds[];
   const int tid = threadIdx.x, nt = blockDim.x;
-  const size_t base = (size_t)blockIdx.x * p.n;
+  const size_t base = (size_t)blockIdx.x * stride;
   if constexpr (PN > 0) {
     const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), p.tw, tid, nt);
     auto ld = [&](int, int, int j) { return in[base + j]; };
@@ -1081,16 +1081,23 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
   return run_pipeline(a, g, d->Z, in, out, T, U, (hipStream_t)stream, pw, ph, tab_bytes(g) ? tabs : nullptr);
 }
 
-extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream) {
-  if (!in || !out || rows < 1) return fail(THZ_E_ARG, "bad fft_rows arguments");
+namespace thz {
+// rows transforms of length n, row r at in/out + r * stride (in place allowed): one launch
+int fft_rows_strided(const void* in, void* out, int rows, int n, size_t stride, int inverse, hipStream_t s) {
+  if (!in || !out || rows < 1 || stride < (size_t)n) return fail(THZ_E_ARG, "bad fft_rows arguments");
   FftPlan p;
   int e = get_plan(n, &p);
   if (e) return e;
   if ((e = ensure_lds_attr())) return e;
-  THZ_POW2_SWITCH(n, fft_rows_kernel, dim3(rows), dim3(threads_for(n)), fft_lds_bytes_io(n), (hipStream_t)stream,
-                  (const float2*)in, (float2*)out, p, inverse);
+  THZ_POW2_SWITCH(n, fft_rows_kernel, dim3(rows), dim3(threads_for(n)), fft_lds_bytes_io(n), s, (const float2*)in,
+                  (float2*)out, p, inverse, stride);
   THZ_LAUNCH_CHECK();
   return THZ_OK;
+}
+}  // namespace thz
+
+extern "C" int thz_fft_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream) {
+  return fft_rows_strided(in, out, rows, n, (size_t)n, inverse, (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -43,6 +43,9 @@ struct KernelTimer {
 
 // Threads per workgroup for a length-n LDS transform.
 // FFT_MAXV values per thread -> n/16 threads (512 for n = 8192, 1024 for n = 16384).
+// rows in-place-capable transforms of length n at row stride `stride` elements (thz_asm.hip)
+int fft_rows_strided(const void* in, void* out, int rows, int n, size_t stride, int inverse, hipStream_t s);
+
 inline int fft_threads(int n) {
   int t = (n + FFT_MAXV - 1) / FFT_MAXV;
   t = (t + 63) / 64 * 64;

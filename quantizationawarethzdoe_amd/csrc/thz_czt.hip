@@ -480,15 +480,9 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
-  // filter spectra FFT_np2(1/h) in place, one row per wavelength
-  for (int c = 0; c < d->C; ++c) {
-    if ((e = thz_fft_rows(ws + a.ftA + (size_t)c * a.tabStride, ws + a.ftA + (size_t)c * a.tabStride, 1,
-                          a.pa.np2, 0, stream)))
-      return e;
-    if ((e = thz_fft_rows(ws + a.ftB + (size_t)c * a.tabStride, ws + a.ftB + (size_t)c * a.tabStride, 1,
-                          a.pb.np2, 0, stream)))
-      return e;
-  }
+  // filter spectra FFT_np2(1/h) in place, one row per wavelength: one launch per axis
+  if ((e = fft_rows_strided(ws + a.ftA, ws + a.ftA, d->C, a.pa.np2, (size_t)a.tabStride, 0, s))) return e;
+  if ((e = fft_rows_strided(ws + a.ftB, ws + a.ftB, d->C, a.pb.np2, (size_t)a.tabStride, 0, s))) return e;
   if (d->adjoint) {  // G [B, C, outW, outH] -> grad_in [B, C, H, W]: column pass first
     KernelTimer kt("czt_adjoint", s);
     THZ_CZT_SWITCH(a.pb.np2, czt_cols_adj, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
