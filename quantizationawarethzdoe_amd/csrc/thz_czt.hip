@@ -20,6 +20,7 @@
 // spectra by the same LDS FFT.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 
 #include "thz_common.hpp"
@@ -97,6 +98,14 @@ __global__ void czt_tables(CztArgs a, float2* __restrict__ ws, int pass) {
   }
 }
 
+// Bluestein length 2560 = 8 5 8 8 (cfg3: m + M - 1 = 2559) as a compile-time mixed plan with
+// 320 threads: the radix-8 stages are one butterfly per thread, the first and last radix match
+// so the forward's spectrum stays in registers for the inverse (as the power-of-two path).
+using CztMx = MxPlan<8, 5, 8, 8>;
+constexpr int CZT_MX_T = 320;
+constexpr int CZT_MX_MB = CztMx::N / CztMx::RL / CZT_MX_T;
+static_assert(CZT_MX_MB * CztMx::RL * CZT_MX_T == CztMx::N, "CZT mixed plan: one last-stage block per thread");
+
 template <int PN>
 struct CztGeo {
   static constexpr int T = PN > 0 ? PN / pow2_v(PN) : 0;
@@ -133,7 +142,17 @@ __global__ void __launch_bounds__(1024) czt_rows(const float2* __restrict__ in, 
     if (q >= 0 && q < M) dst[blk(q, h, a.H)] = cmul(v, post[q]);
   };
   int tid = threadIdx.x;
-  if constexpr (PN > 0) {
+  if constexpr (PN == CztMx::N) {
+    const auto twr = CztMx::twiddles<CZT_MX_T>(pl.tw, tid);
+    float2 sp[CZT_MX_MB][CztMx::RL];
+    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
+    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
+    CztMx::run<false, CZT_MX_T>(lds, twr, tid, ld0, sv0);
+    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
+    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
+    __syncthreads();  // the forward's LDS reads are done before the inverse's first exchange
+    CztMx::run<true, CZT_MX_T>(lds, twr, tid, ld1, sv1);
+  } else if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = CztGeo<PN>::T;
     constexpr int RL = S::radix(S::NST - 1, false);
@@ -191,7 +210,17 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
     }
   };
   int tid = threadIdx.x;
-  if constexpr (PN > 0) {
+  if constexpr (PN == CztMx::N) {
+    const auto twr = CztMx::twiddles<CZT_MX_T>(pl.tw, tid);
+    float2 sp[CZT_MX_MB][CztMx::RL];
+    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
+    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
+    CztMx::run<false, CZT_MX_T>(lds, twr, tid, ld0, sv0);
+    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
+    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
+    __syncthreads();  // the forward's LDS reads are done before the inverse's first exchange
+    CztMx::run<true, CZT_MX_T>(lds, twr, tid, ld1, sv1);
+  } else if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = CztGeo<PN>::T;
     constexpr int RL = S::radix(S::NST - 1, false);
@@ -333,11 +362,30 @@ static int np2_of(int x) {
   return p;
 }
 
+// THZ_CZT_NICE=1: the shortest 2^a 3^b 5^c length >= mp + 1 instead of the power of two. Any
+// N >= mp + 1 gives the same Bluestein output (the kept rows see g[t] for t in [1, mp] only, so
+// nothing wraps); non-power-of-two lengths take the runtime-plan kernels.
+static int nice_of(int x) {
+  int best = np2_of(x);
+  for (int a = 1; a <= best; a *= 2)
+    for (int b = a; b <= best; b *= 3)
+      for (int c = b; c <= best; c *= 5)
+        if (c >= x && c < best) best = c;
+  return best;
+}
+
 static void make_pass(BluePass* p, int m, int M, double lo, double hi) {
   p->m = m;
   p->M = M;
   const int mp = m + M - 1;
-  p->np2 = np2_of(mp);
+  static const bool nice = [] { const char* e = getenv("THZ_CZT_NICE"); return e && atoi(e) > 0; }();
+  // THZ_CZT_MX=1 (off by default): a pass whose power of two would be 4096 but fits 2560 takes
+  // the compile-time 2560-point plan of the forward kernels (adjoints run the runtime plan).
+  // Parity-green, but slower at cfg3: czt_rows 1.48 ms against 1.10 ms for the split-exchange
+  // 4096-point path, so the 37.5 % shorter transform does not pay yet.
+  static const bool mx = [] { const char* e = getenv("THZ_CZT_MX"); return e && atoi(e) > 0; }();
+  p->np2 = nice ? nice_of(mp + 1) : np2_of(mp);
+  if (mx && !nice && p->np2 > CztMx::N && mp + 1 <= CztMx::N) p->np2 = CztMx::N;
   const int Lh = m + std::max(M - 1, m - 1);  // arange(-m+1, max(M-1, m-1)+1)
   p->ntab = std::min(mp + 1, Lh);
   p->f1 = lo;
@@ -416,6 +464,10 @@ static int czt_pow2(int n) {
     default: hipLaunchKernelGGL(KER<0>, __VA_ARGS__); break;                             \
   }
 
+#define THZ_CZT_SWITCH_FWD(n, KER, ...)                                                 \
+  if ((n) == CztMx::N) hipLaunchKernelGGL(KER<CztMx::N>, __VA_ARGS__);                   \
+  else THZ_CZT_SWITCH(n, KER, __VA_ARGS__)
+
 static int czt_lds_attr() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
@@ -429,7 +481,8 @@ static int czt_lds_attr() {
         (const void*)czt_rows_adj<0>,  (const void*)czt_rows_adj<1024>, (const void*)czt_rows_adj<2048>,
         (const void*)czt_rows_adj<4096>, (const void*)czt_rows_adj<8192>, (const void*)czt_rows_adj<16384>,
         (const void*)czt_cols_adj<0>,  (const void*)czt_cols_adj<1024>, (const void*)czt_cols_adj<2048>,
-        (const void*)czt_cols_adj<4096>, (const void*)czt_cols_adj<8192>, (const void*)czt_cols_adj<16384>};
+        (const void*)czt_cols_adj<4096>, (const void*)czt_cols_adj<8192>, (const void*)czt_cols_adj<16384>,
+        (const void*)czt_rows<CztMx::N>, (const void*)czt_cols<CztMx::N>};
     for (const void* k : ks) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       if (e != hipSuccess) err = e;
@@ -440,6 +493,8 @@ static int czt_lds_attr() {
 }
 
 static int threads_pow2_or(int n) { return czt_pow2(n) ? n / pow2_v(n) : fft_threads(n); }
+// forward kernels: the compile-time 2560 plan runs CZT_MX_T threads
+static int threads_fwd(int n) { return n == CztMx::N ? CZT_MX_T : threads_pow2_or(n); }
 
 }  // namespace thz
 
@@ -496,14 +551,14 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   }
   {
     KernelTimer kt("czt_rows", s);
-    THZ_CZT_SWITCH(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
+    THZ_CZT_SWITCH_FWD(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_fwd(a.pa.np2)),
                    fft_lds_bytes_io(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
   {
     KernelTimer kt("czt_cols", s);
-    THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
+    THZ_CZT_SWITCH_FWD(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_fwd(a.pb.np2)),
                    fft_lds_bytes_io(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
     THZ_LAUNCH_CHECK();
     kt.stop();

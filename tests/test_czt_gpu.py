@@ -70,3 +70,37 @@ def test_czt_backward_vs_oracle_autograd(H, W, out, C):
         torch.set_default_dtype(old)
     assert gx.shape == xd.shape
     assert rel_l2(gx.cpu().numpy(), ro_g.numpy()) <= 1e-3, rel_l2(gx.cpu().numpy(), ro_g.numpy())
+
+
+@pytest.mark.parametrize("H,W,out,C", [(2048, 2048, 512, 2), (1800, 2048, 400, 1)])
+def test_czt_mixed_radix_2560_vs_oracle(H, W, out, C):
+    """cfg3-sized CZT (m + M - 1 <= 2559): forward and backward vs the fp64 oracle, rel-L2 <= 1e-3.
+    By default both Bluestein passes run 4096-point transforms.  Under THZ_CZT_MX=1 they run the
+    2560 = 8 5 8 8 plans instead (compile-time in the forward kernels, runtime in the adjoints).
+    This test covers both settings; the env var is read once per process."""
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.CZT_Prop import CZT_prop
+    rng = np.random.default_rng(H + out)
+    x = (rng.standard_normal((1, C, H, W)) + 1j * rng.standard_normal((1, C, H, W))).astype(np.complex64)
+    freqs = [240 + 60 * c for c in range(C)]
+    wl = [C0 / (f * 1e9) for f in freqs]
+    dev = torch.device("cuda:0")
+    xd = torch.from_numpy(x).to(dev).requires_grad_(True)
+    field = ElectricField(xd, wavelengths=wl if C > 1 else wl[0], spacing=[0.5e-3, 0.5e-3], device=dev)
+    o = CZT_prop(z_distance=0.2, device=dev)(field, out, out, 0.35e-3, 0.35e-3).data
+    g = (rng.standard_normal(o.shape) + 1j * rng.standard_normal(o.shape)).astype(np.complex64)
+    gx, = torch.autograd.grad(o, xd, grad_outputs=torch.from_numpy(g).to(dev))
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        xo = torch.from_numpy(x).to(torch.complex128).requires_grad_(True)
+        sp = torch.tensor([0.5e-3, 0.5e-3], dtype=torch.float32).double()
+        ro = orc.czt_forward(xo, wavelengths(freqs, True), sp, 0.2, out, out,
+                             float(torch.tensor(0.35e-3, dtype=torch.float32)),
+                             float(torch.tensor(0.35e-3, dtype=torch.float32)))
+        ro_g, = torch.autograd.grad(ro, xo, grad_outputs=torch.from_numpy(g).to(torch.complex128))
+    finally:
+        torch.set_default_dtype(old)
+    ef = rel_l2(o.detach().cpu().numpy(), ro.detach().numpy())
+    eb = rel_l2(gx.cpu().numpy(), ro_g.numpy())
+    assert ef <= 1e-3 and eb <= 1e-3, (ef, eb)
