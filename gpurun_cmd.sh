@@ -1,6 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash scripts/gpu_step.sh 300 gpurun_out/gpu_tests_czt_def.log python -u -m pytest tests/test_czt_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread &&
-THZ_CZT_MX=1 bash scripts/gpu_step.sh 300 gpurun_out/gpu_tests_czt_mx1.log python -u -m pytest tests/test_czt_gpu.py -x -q -m gpu --timeout 120 --timeout-method thread &&
-timeout -k 10 300 python3 scripts/czt_prof.py 10 > gpurun_out/czt_def.log 2>&1
+bash scripts/gpu_step.sh 600 gpurun_out/final_gpu_tests.log python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread &&
+bash scripts/gpu_step.sh 200 gpurun_out/final_smoke.log python -c "import __graft_entry__ as g; g.smoke(); print('SMOKE OK')" &&
+bash scripts/gpu_step.sh 300 gpurun_out/final_bench.log python bench.py
