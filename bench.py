@@ -60,27 +60,32 @@ def z_planes(rank, world):
     return [float(zs[i]) for i in shard_planes(total, rank, world)]
 
 
-def cpu_baseline(budget_s=12.0, max_planes=8):
-    """The oracle (PyTorch-CPU restatement of the reference op sequence, oracle/thz_oracle.py)
-    timed on this host's cores on a bounded sample of the same workload (whole 4096^2 planes)."""
+def cpu_baseline(budget_s=20.0, max_planes=8):
+    """The oracle (PyTorch-CPU restatement of the reference op sequence, oracle/thz_oracle.py:105-119:
+    per-call transfer-function rebuild, four fftshifts, full P x P FFTs) timed on this host's cores on
+    a bounded sample of the same workload: whole 4096^2 planes of the 64-plane sweep, spread over
+    the sweep, until max_planes or the time budget (``--cpu-planes 64`` times the whole sweep)."""
     from oracle import thz_oracle as orc
     threads = torch.get_num_threads()
     x = gaussian(N_FIELD, DX, WAIST, "cpu")
     lam = torch.tensor([C0 / FREQ], dtype=torch.float32)
     sp = torch.tensor([DX, DX], dtype=torch.float32)
     zs = z_planes(0, 1)
+    stride = max(1, len(zs) // max(1, max_planes))
     orc.asm_forward(x[..., :512, :512], lam, sp, zs[0], 1)  # warm MKL
     t0 = time.perf_counter()
     n = 0
     while n < max_planes:
-        orc.asm_forward(x, lam, sp, zs[n % len(zs)], 1)
+        orc.asm_forward(x, lam, sp, zs[(n * stride) % len(zs)], 1)
         n += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "propagations/s", "cores": threads, "kind": "port",
-            "sample": f"{n} planes of the cfg2 workload (4096^2 -> P=8192, exact band limit) through "
-                      f"oracle.thz_oracle.asm_forward, torch-CPU fp32, {threads} threads, {dt:.1f} s"}
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"{n} of the 64 planes of the cfg2 workload (4096^2 -> P=8192, exact band limit, z every "
+                      f"{stride} planes of the 20-120 mm sweep) through oracle.thz_oracle.asm_forward, torch-CPU "
+                      f"fp32, {threads} threads, {dt:.1f} s"}
 
 
 def bench_czt(dev, rank, world, steps=10, warmup=2, dist=None):
@@ -185,7 +190,8 @@ def bench_donn(dev, rank, world, steps=20, warmup=3, dist=None):
 
 
 def load_traffic():
-    """HBM bytes per launch of the dominant kernel from the committed rocprofv3 PMC summary."""
+    """HBM bytes per launch of each kernel from the committed rocprofv3 PMC summary
+    (scripts/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) x 1 KiB, the gfx950 correction)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -196,6 +202,134 @@ def load_traffic():
         return None
 
 
+def cpu_model():
+    """Host CPU model name (the lscpu "Model name" line, read from /proc/cpuinfo)."""
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for ln in fh:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def check_plane(plane, z):
+    """Outside the timed region: one output plane of the bench vs the REFERENCE's own fp64 output
+    signature of the same workload (tests/golden/cfg2_check.npz, made by tests/golden/
+    gen_cfg2_check.py in the build container): energy, E[::64, ::64] and row 2048, rel-L2 <= 1e-4."""
+    import numpy as np
+    path = os.path.join(ROOT, "tests", "golden", "cfg2_check.npz")
+    with np.load(path, allow_pickle=False) as G:
+        zs = [float(v) for v in G["z"]]
+        k = min(range(len(zs)), key=lambda i: abs(zs[i] - z))
+        if abs(zs[k] - z) > 1e-9:
+            return None
+        sub = plane[::64, ::64].cpu().numpy().astype(np.complex128)
+        row = plane[2048].cpu().numpy().astype(np.complex128)
+        energy = float((plane.abs().double() ** 2).sum())
+
+        def rel(a, b):
+            return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+        r = {"z_m": z, "rel_sub": rel(sub, G[f"p{k}__sub64"]), "rel_row": rel(row, G[f"p{k}__row64"]),
+             "rel_energy": abs(energy - float(G[f"p{k}__energy64"])) / float(G[f"p{k}__energy64"])}
+    r["ok"] = bool(r["rel_sub"] <= 1e-4 and r["rel_row"] <= 1e-4 and r["rel_energy"] <= 1e-5)
+    return r
+
+
+class Ranks:
+    """One process per GPU (torch.distributed.run sets RANK / LOCAL_RANK / WORLD_SIZE): the barrier and
+    the max-over-ranks reduction of the timed region.  ``dry_run``: every rank on the CPU over gloo,
+    the propagation stubbed (tests/test_distributed_cpu.py rehearses the orchestration this way)."""
+
+    def __init__(self, dry_run=False):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.dry_run = dry_run
+        # rehearsing N > 1 on a one-GPU box: every rank on cuda:0 (gloo)
+        if os.environ.get("THZ_BENCH_SAME_DEVICE"):
+            local = 0
+        backend = "gloo" if dry_run else os.environ.get("THZ_BENCH_BACKEND", "nccl")
+        if dry_run:
+            self.dev = torch.device("cpu")
+        else:
+            self.dev = torch.device("cuda", local)
+            torch.cuda.set_device(self.dev)
+        if self.world > 1:
+            import torch.distributed as dist
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(backend)
+            self.dist = dist
+
+    def sync(self):
+        if not self.dry_run:
+            torch.cuda.synchronize()
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max(self, v):
+        if self.dist is None:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def timed(step, steps, warmup, ranks, on_start=None):
+    """W untimed warmup steps, then EXACTLY K timed steps bracketed by a barrier + synchronize on
+    both sides; returns the max over ranks of the elapsed wall time."""
+    for _ in range(warmup):
+        step()
+    ranks.sync()
+    if on_start:
+        on_start()
+    ranks.barrier()
+    ranks.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    ranks.sync()
+    ranks.barrier()
+    return ranks.max(time.perf_counter() - t0)
+
+
+def launch_ranks(args):
+    """``--gpus N`` without a launcher: start N ranks as a child torch.distributed.run (before anything
+    touches the GPU; never an exec) and exit with its code.  Under a launcher, N must equal WORLD_SIZE."""
+    if "WORLD_SIZE" in os.environ:
+        if int(os.environ["WORLD_SIZE"]) != args.gpus:
+            sys.stderr.write(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}\n")
+            sys.exit(2)
+        return
+    if args.gpus <= 1:
+        return
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.call(cmd))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,32 +337,41 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--z-chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-planes", type=int, default=8, help="cpu_baseline sample size (whole 4096^2 planes)")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="cpu_baseline time budget, seconds")
     ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 / cfg5 secondary measurements")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rehearse the rank orchestration on the CPU (gloo, propagation stubbed, no GPU)")
     args = ap.parse_args()
+    launch_ranks(args)
+    ranks = Ranks(args.dry_run)
+    rank, world, dev = ranks.rank, ranks.world, ranks.dev
+    zs = z_planes(rank, world)
+    if args.dry_run:
+        done = []
+        seen = torch.zeros(1, dtype=torch.float64)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # test knobs for rehearsing N > 1 on a one-GPU box: every rank on cuda:0 over gloo
-    if os.environ.get("THZ_BENCH_SAME_DEVICE"):
-        local = 0
-    backend = os.environ.get("THZ_BENCH_BACKEND", "nccl")
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+        def step():
+            done.append(len(zs))
+            seen.add_(sum(zs))
+        elapsed = timed(step, args.steps, args.warmup, ranks)
+        planes = Z_PER_RANK * world * args.steps
+        cover = sorted(i for r in ranks.gather(shard_planes(Z_PER_RANK * world, rank, world)) for i in r)
+        lam_cover = sorted(i for r in ranks.gather(shard_planes(32, rank, world)) for i in r)  # cfg3 λ shards
+        batch_cover = sorted(i for r in ranks.gather(shard_planes(256, rank, world)) for i in r)  # cfg5 batch
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": round(planes / elapsed, 2), "unit": "propagations/s",
+                              "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                              "planes_per_rank_step": done[-1], "planes_covered": cover,
+                              "wavelengths_covered": lam_cover, "samples_covered": batch_cover,
+                              "elapsed_max_s": elapsed}), flush=True)
+        ranks.close()
+        return
 
     from quantizationawarethzdoe_amd import _lib
     from quantizationawarethzdoe_amd.propagation import asm_apply, asm_plan_info
 
     x = gaussian(N_FIELD, DX, WAIST, dev)
-    zs = z_planes(rank, world)
     lam = [float(torch.tensor(C0 / FREQ, dtype=torch.float32))]
     sp = [float(torch.tensor(DX, dtype=torch.float32))] * 2
     pad = N_FIELD // 2
@@ -237,27 +380,16 @@ def main():
     def step():
         asm_apply(x, lam, sp, zs, pad, pad, True, 1, z_chunk=args.z_chunk, out=out)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    _lib.timing_reset()
-    _lib.timing_enable(True)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    def start_timing():
+        _lib.timing_reset()
+        _lib.timing_enable(True)
+    elapsed = timed(step, args.steps, args.warmup, ranks, on_start=start_timing)
     _lib.timing_enable(False)
     kern = {k: _lib.timing_read(k) for k in ("asm_rows_fwd", "asm_cols", "asm_rows_inv")}
-    if dist is not None:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    # self-check outside the timed region: this rank's first plane (z = 20 mm on rank 0) and, when
+    # it is in this rank's share, the sweep's last (120 mm), vs the reference's fp64 signature
+    checks = [c for c in (check_plane(out[0, 0, 0], zs[0]), check_plane(out[-1, 0, 0], zs[-1])) if c]
+    checks_ok = all(ranks.gather(all(c["ok"] for c in checks)))
 
     planes = Z_PER_RANK * world * args.steps
     value = planes / elapsed
@@ -276,22 +408,30 @@ def main():
              "asm_rows_inv": 8 * zc * (H * Pw + H * W)}
     pruned = {"asm_rows_fwd": 8 * (H * W + ncols * H), "asm_cols": 8 * (ncols * H + zc * ncols * H),
               "asm_rows_inv": 8 * (zc * ncols * H + zc * H * W)}
+    traffic = load_traffic() or {}
     stats = {}
     for k, (ms, n) in kern.items():
         if n:
             avg = ms / n
             stats[k] = {"avg_ms": avg, "launches": n, "alg_bytes": model[k], "pruned_bytes": pruned[k],
                         "gbs": model[k] / (avg * 1e-3) / 1e9, "gbs_pruned": pruned[k] / (avg * 1e-3) / 1e9}
+            if traffic.get(k):
+                stats[k]["pmc_bytes"] = traffic[k]
+                stats[k]["gbs_pmc"] = traffic[k] / (avg * 1e-3) / 1e9
     dom = max(stats, key=lambda k: stats[k]["avg_ms"] * stats[k]["launches"]) if stats else None
     total_alg = sum(pruned[k] * stats[k]["launches"] for k in stats) / args.steps
-    traffic = load_traffic()
+    total_pmc = (sum(traffic[k] * stats[k]["launches"] for k in stats) / args.steps
+                 if all(traffic.get(k) for k in stats) else None)
     roof = roof_pruned = None
     if dom:
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(stats[dom]["gbs"], 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(stats[dom]["gbs"] / HBM_PEAK_GBS, 4),
-                "traffic": (traffic or {}).get(dom),
+                "traffic": traffic.get(dom),
+                "traffic_gbs": round(stats[dom]["gbs_pmc"], 1) if "gbs_pmc" in stats[dom] else None,
                 "alg_bytes_per_launch": model[dom], "avg_launch_ms": round(stats[dom]["avg_ms"], 4),
-                "bytes_model": "SURVEY §8(d) 3-pass byte model, z_chunk planes per launch"}
+                "bytes_model": "SURVEY §8(d) 3-pass byte model, z_chunk planes per launch; traffic = PMC "
+                               "(2 FETCH_SIZE + WRITE_SIZE) bytes per launch (profiles/pmc_traffic.json), "
+                               "traffic_gbs = traffic / live avg launch time"}
         roof_pruned = {"kernel": dom, "achieved": round(stats[dom]["gbs_pruned"], 1), "peak": HBM_PEAK_GBS,
                        "unit": "GB/s", "frac": round(stats[dom]["gbs_pruned"] / HBM_PEAK_GBS, 4),
                        "alg_bytes_per_launch": pruned[dom],
@@ -309,25 +449,29 @@ def main():
                    "band_columns": ncols, "z_chunk": zc, "parallelism": f"z-shard x{world}"},
         "hbm_gbs_band_pruned": round(total_alg * args.steps / elapsed / 1e9 * world, 1),
         "hbm_gbs_survey_model": round(step_model * args.steps / elapsed / 1e9 * world, 1),
+        "hbm_gbs_pmc": round(total_pmc * args.steps / elapsed / 1e9 * world, 1) if total_pmc else None,
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in stats.items()},
         "roofline": roof,
         "roofline_band_pruned": roof_pruned,
+        "output_check": {"ok": checks_ok, "planes": checks},
     }
     if not args.headline_only:
         # secondary workloads never take the headline line down with them
         line["secondary"] = {}
         for key, fn in (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat), ("cfg5_donn", bench_donn)):
             try:
-                line["secondary"][key] = fn(dev, rank, world, dist=dist)
+                line["secondary"][key] = fn(dev, rank, world, dist=ranks.dist)
             except Exception as e:  # noqa: BLE001 -- reported in the JSON line
                 line["secondary"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline()
+        line["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.cpu_planes)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    ranks.close()
+    if not checks_ok:
+        sys.stderr.write(f"bench.py: output check FAILED: {checks}\n")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -119,6 +119,25 @@ def asm_forward(data, wavelengths, spacing, z, padding_scale=1, do_padding=True,
     return y
 
 
+def asm_forward_planes(data, wavelengths, spacing, zs, padding_scale=1, bandlimit_type="exact"):
+    """The multi-z sweep of experiment_extend_depth_of_focus.ipynb:229,255-256 (``asm.z = z;
+    asm(field)`` per plane): yields (z, asm_forward(data, .., z, ..)) for each z.  ft2(pad x) does not
+    depend on z, so it is computed once -- the same operations as the per-plane call, hence the
+    same values, at a fraction of the cost for the full-size (P = 8192) parity tests."""
+    rdt = _rdt(data)
+    B, C, H, W = data.shape
+    ph, pw, Ph, Pw = asm_padding(H, W, padding_scale, True)
+    spec = ft2(torch.nn.functional.pad(data, (pw, pw, ph, ph)))
+    top = int(round((Ph - H) / 2.0))
+    left = int(round((Pw - W) / 2.0))
+    for z in zs:
+        Hf = asm_transfer_function(Ph, Pw, torch.as_tensor(wavelengths), spacing[0], spacing[1], z, True,
+                                   bandlimit_type, rdt)
+        y = ift2(spec * Hf)[..., top:top + H, left:left + W]
+        del Hf
+        yield z, y
+
+
 # ---------------------------------------------------------------------------------------------
 # CZT  (Props/CZT_Prop.py)
 # ---------------------------------------------------------------------------------------------

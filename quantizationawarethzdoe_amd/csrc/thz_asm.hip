@@ -302,8 +302,9 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
     const float kl = TWO_PI_F / lam;
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
-    if ((int)threadIdx.x < z_hi - z_lo) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + threadIdx.x]);
+    // strided over the chunk: a z_chunk may exceed the workgroup (64 threads at P = 1024)
+    for (int zz = threadIdx.x; zz < z_hi - z_lo; zz += nt) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + zz]);
       int lo = -1, hi = PN / 2 + 1;
       const int bl = a.bl, P = a.Ph;
       const float dx = a.dx;
@@ -315,7 +316,7 @@ __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K
           else hi = mid;
         }
       }
-      mz[threadIdx.x] = lo;
+      mz[zz] = lo;
     }
     // sqrt(k^2 - Kx^2 - Ky^2) of the elements this thread holds: z-independent, computed once
     // per column (the per-z work is then one product and one sincos per element)

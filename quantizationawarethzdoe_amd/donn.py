@@ -21,7 +21,6 @@ import os
 
 import numpy as np
 import torch
-import torch.distributed as dist
 import torch.nn as nn
 
 from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
@@ -139,13 +138,14 @@ class DONNTrainer:
     the batch and its targets are copied into static device buffers before each replay.
     """
 
-    def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True):
+    def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True, loss_fn=None):
         from quantizationawarethzdoe_amd.qat import GradientAllReduce
         self.model = model
         self.targets = targets.to(model.device).float().contiguous()
         self.max_itrs = max_itrs
         self.graph = graph
         self.chained = chained
+        self.loss_fn = loss_fn
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph)
         self.allreduce = GradientAllReduce(self.params, group=group)
@@ -158,9 +158,23 @@ class DONNTrainer:
                 d._dyn = self.dyn
 
     def _loss(self, u, target, frac):
-        from quantizationawarethzdoe_amd.optics import intensity_mse
+        if self.loss_fn is None:
+            from quantizationawarethzdoe_amd.optics import intensity_mse
+            self.loss_fn = intensity_mse
         out = self.model(u, frac, chained=self.chained)
-        return intensity_mse(out.data, target)
+        return self.loss_fn(out.data, target)
+
+    # the step in two phases around the one collective (qat.QATTrainer's scheme): the eager step
+    # and the captured graphs run the same functions
+    def _fb(self, u, target, frac):
+        loss = self._loss(u, target, frac)
+        loss.backward()
+        self.allreduce.pack()
+        return loss
+
+    def _opt(self):
+        self.allreduce.unpack()
+        self.optimizer.step()
 
     def step(self, u, labels, iter_frac=None):
         """One iteration on images ``u`` [B, 1, H, W] (float, this rank's share) and int64 ``labels`` [B]."""
@@ -170,33 +184,14 @@ class DONNTrainer:
         if self.graph:
             loss = self._graph_step(u, target, frac)
         else:
-            loss = self._loss(u, target, frac)
             self.optimizer.zero_grad(set_to_none=False)
-            loss.backward()
-            self.allreduce()
-            self.optimizer.step()
+            loss = self._fb(u, target, frac)
+            self.allreduce.reduce()
+            self._opt()
         self.itr += 1
         return loss
 
     # -- graph path ----------------------------------------------------------------------------
-    def _pack(self):
-        off = 0
-        for p in self.params:
-            k = p.numel()
-            if p.grad is None:
-                self.allreduce.flat[off:off + k].zero_()
-            else:
-                self.allreduce.flat[off:off + k].copy_(p.grad.reshape(-1))
-            off += k
-
-    def _unpack(self):
-        off = 0
-        for p in self.params:
-            k = p.numel()
-            if p.grad is not None:
-                p.grad.copy_(self.allreduce.flat[off:off + k].view_as(p))
-            off += k
-
     def _capture(self, frac):
         su, st = self._static
         p0 = [p.detach().clone() for p in self.params]
@@ -207,8 +202,8 @@ class DONNTrainer:
         with torch.cuda.stream(side):
             for _ in range(2):  # allocator, autograd and Adam's lazy state, outside the capture
                 self.optimizer.zero_grad(set_to_none=True)
-                self._loss(su, st, frac).backward()
-                self.optimizer.step()
+                self._fb(su, st, frac)
+                self._opt()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         with torch.no_grad():  # the warm-up must not move the training trajectory
@@ -222,14 +217,9 @@ class DONNTrainer:
         self.optimizer.zero_grad(set_to_none=True)
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
-            loss = self._loss(su, st, frac)
-            loss.backward()
-            if self.allreduce.world > 1:
-                self._pack()
+            loss = self._fb(su, st, frac)
         with torch.cuda.graph(g_opt):
-            if self.allreduce.world > 1:
-                self._unpack()
-            self.optimizer.step()
+            self._opt()
         return g_fb, g_opt, loss
 
     def _graph_step(self, u, target, frac):
@@ -246,9 +236,7 @@ class DONNTrainer:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
         g_fb.replay()
-        if self.allreduce.world > 1:
-            dist.all_reduce(self.allreduce.flat, op=dist.ReduceOp.SUM, group=self.allreduce.group)
-            self.allreduce.flat.mul_(1.0 / self.allreduce.world)
+        self.allreduce.reduce()
         g_opt.replay()
         return loss
 

@@ -107,7 +107,11 @@ class GradientAllReduce:
     """Average the gradients of ``params`` over the process group with ONE flat all-reduce.
 
     10 KB for cfg4 (50 x 50 fp32): latency-bound, so a single bucket; the flat buffer is
-    allocated once and reused every step.
+    allocated once and reused every step.  The three phases are separate so the trainers can
+    put ``pack`` at the end of the captured forward/backward graph, ``reduce`` (the collective)
+    between the graph replays and ``unpack`` at the head of the optimiser graph -- the same
+    calls the eager step makes, so the CPU gloo tests run the exact placement the HIP-graph
+    path replays.  All three are no-ops at world size 1.
     """
 
     def __init__(self, params, group=None):
@@ -118,7 +122,8 @@ class GradientAllReduce:
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
 
-    def __call__(self):
+    def pack(self):
+        """Gradients -> the flat bucket (a parameter without a gradient contributes zeros)."""
         if self.world == 1:
             return
         off = 0
@@ -129,8 +134,18 @@ class GradientAllReduce:
             else:
                 self.flat[off:off + k].copy_(p.grad.reshape(-1))
             off += k
+
+    def reduce(self):
+        """The one collective of the step: sum over ranks, then / world."""
+        if self.world == 1:
+            return
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
+
+    def unpack(self):
+        """The averaged bucket -> every parameter's gradient."""
+        if self.world == 1:
+            return
         off = 0
         for p in self.params:
             k = p.numel()
@@ -140,6 +155,11 @@ class GradientAllReduce:
             else:
                 p.grad.copy_(g)
             off += k
+
+    def __call__(self):
+        self.pack()
+        self.reduce()
+        self.unpack()
 
 
 class QATTrainer:
@@ -155,11 +175,13 @@ class QATTrainer:
     stream differs from the eager path (same distribution, different draws).
     """
 
-    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False):
+    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False, loss_fn=None):
         self.system = system
         self.target = target.to(system.device).float().contiguous()
         self.max_itrs = max_itrs
         self.graph = graph
+        # loss(out_field_data, target): the fused HIP |E|^2 -> normalize -> MSE by default
+        self.loss_fn = loss_fn or _optics.intensity_mse
         self.optimizer = torch.optim.Adam(system.parameters(), lr=lr, capturable=graph)
         self.allreduce = GradientAllReduce(list(system.parameters()), group=group)
         self.itr = 0
@@ -171,27 +193,32 @@ class QATTrainer:
     def _frac(self, iter_frac):
         return self.itr / self.max_itrs if iter_frac is None else iter_frac
 
+    # The step in two phases around the one collective; the eager step and the captured graphs
+    # run the same two functions (fwd/bwd + pack | all-reduce | unpack + Adam).
+    def _fb(self, frac):
+        out = self.system(frac)
+        loss = self.loss_fn(out.data, self.target)
+        loss.backward()
+        self.allreduce.pack()
+        return loss
+
+    def _opt(self):
+        self.allreduce.unpack()
+        self.optimizer.step()
+
     def step(self, iter_frac=None):
         frac = self._frac(iter_frac)
         if self.graph:
             loss = self._graph_step(frac)
         else:
-            out = self.system(frac)
-            loss = _optics.intensity_mse(out.data, self.target)
             self.optimizer.zero_grad(set_to_none=False)
-            loss.backward()
-            self.allreduce()
-            self.optimizer.step()
+            loss = self._fb(frac)
+            self.allreduce.reduce()
+            self._opt()
         self.itr += 1
         return loss
 
     # -- graph path ----------------------------------------------------------------------------
-    def _fwd_bwd(self, frac):
-        out = self.system(frac)
-        loss = _optics.intensity_mse(out.data, self.target)
-        loss.backward()
-        return loss
-
     def _capture(self, frac):
         params = self.allreduce.params
         # warm-up steps (allocator, autograd, Adam's lazy state) must not change the training
@@ -204,8 +231,8 @@ class QATTrainer:
         with torch.cuda.stream(side):
             for _ in range(2):
                 self.optimizer.zero_grad(set_to_none=True)
-                self._fwd_bwd(frac)
-                self.optimizer.step()
+                self._fb(frac)
+                self._opt()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         with torch.no_grad():
@@ -219,21 +246,9 @@ class QATTrainer:
         self.optimizer.zero_grad(set_to_none=True)
         g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_fb):
-            loss = self._fwd_bwd(frac)
-            if self.allreduce.world > 1:
-                off = 0
-                for p in params:
-                    k = p.numel()
-                    self.allreduce.flat[off:off + k].copy_(p.grad.reshape(-1))
-                    off += k
+            loss = self._fb(frac)
         with torch.cuda.graph(g_opt):
-            if self.allreduce.world > 1:
-                off = 0
-                for p in params:
-                    k = p.numel()
-                    p.grad.copy_(self.allreduce.flat[off:off + k].view_as(p))
-                    off += k
-            self.optimizer.step()
+            self._opt()
         return g_fb, g_opt, loss
 
     def _graph_step(self, frac):
@@ -244,9 +259,7 @@ class QATTrainer:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
         g_fb.replay()
-        if self.allreduce.world > 1:
-            dist.all_reduce(self.allreduce.flat, op=dist.ReduceOp.SUM, group=self.allreduce.group)
-            self.allreduce.flat.mul_(1.0 / self.allreduce.world)
+        self.allreduce.reduce()
         g_opt.replay()
         return loss
 
@@ -255,7 +268,8 @@ class QATTrainer:
         losses = []
         for _ in range(steps):
             loss = self.step()
-            losses.append(loss.detach())
+            # graph replays overwrite the captured loss tensor in place: keep a copy per step
+            losses.append(loss.detach().clone())
             if log_every and (self.itr - 1) % log_every == 0:
                 log(f"The iteration : {self.itr - 1}, Loss: {float(loss):.6g}")
         torch.cuda.synchronize()

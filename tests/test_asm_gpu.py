@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import thz_oracle as orc
-from tests.golden_io import arrays, manifest, rel_l2, spacing, wavelengths
+from tests.golden_io import GOLDEN, arrays, manifest, rel_l2, spacing, wavelengths
 
 pytestmark = pytest.mark.gpu
 M = manifest()
@@ -152,6 +152,97 @@ def test_asm_full_size_properties():
     e_in = float((r.abs().double() ** 2).sum())
     e_out = float((o2.abs().double() ** 2).sum())
     assert e_out <= e_in * (1 + 1e-5)
+
+
+def _cfg2_input(dev):
+    """The bench.py cfg2 input: a 4096^2 Gaussian beam (w 50 mm, 300 GHz, dx 0.25 mm) made by the
+    device kernel (LightSource/Gaussian_beam.py:88-160)."""
+    from quantizationawarethzdoe_amd.optics import gaussian_beam
+    lam = float(torch.tensor(C0 / 300e9, dtype=torch.float32))
+    return gaussian_beam(4096, 4096, 0.25e-3, 0.25e-3, [lam], [50e-3], [50e-3], device=dev), lam
+
+
+def test_asm_cfg2_timed_path_vs_oracle():
+    """The exact kernels the headline bench times: asm_cols<8192> with a 32-plane z-chunk (spectrum
+    reused across z in registers, per-z kept-row bisection), the kfull / kparts z-range split of
+    the last dispatch round, and a tail chunk of 8 planes.  40 planes over 20-120 mm (the bench
+    sweep's range, experiment_extend_depth_of_focus.ipynb:229); the first and last plane of each
+    chunk vs the fp32 oracle (<= 1e-4 rel-L2), and the sweep's end planes (z = 20 mm and 120 mm
+    exactly) vs the REFERENCE's own fp64 output signature (tests/golden/cfg2_check.npz: energy,
+    E[::64, ::64], row 2048; <= 1e-4, the reference's own fp32 error there is 4e-6 / 2.3e-5)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_plan_info
+    dev = _dev()
+    x, lam = _cfg2_input(dev)
+    sp = [float(torch.tensor(0.25e-3, dtype=torch.float32))] * 2
+    zs = [float(v) for v in torch.linspace(20e-3, 120e-3, 40, dtype=torch.float64)]
+    ncols, zc = asm_plan_info(1, 1, 4096, 4096, 2048, 2048, True, 1, [lam], sp, zs, 32)
+    assert zc == 32 and ncols < 8192
+    out = asm_apply(x, [lam], sp, zs, 2048, 2048, True, 1, z_chunk=32)
+    assert out.shape == (40, 1, 1, 4096, 4096)
+    check = [0, 31, 32, 39]
+    got = {k: out[k, 0, 0].cpu().numpy() for k in check}
+    del out
+    xc = x.cpu()
+    with torch.no_grad():
+        refs = orc.asm_forward_planes(xc, torch.tensor([lam], dtype=torch.float32), torch.tensor(sp),
+                                      [zs[k] for k in check], 1)
+        for k, (_, ref) in zip(check, refs):
+            e = rel_l2(got[k], ref[0, 0].numpy())
+            assert e <= 1e-4, (k, zs[k], e)
+    G = np.load(f"{GOLDEN}/cfg2_check.npz")
+    for k, p in ((0, 0), (39, 1)):
+        g = got[k].astype(np.complex128)
+        assert rel_l2(g[::64, ::64], G[f"p{p}__sub64"]) <= 1e-4
+        assert rel_l2(g[2048], G[f"p{p}__row64"]) <= 1e-4
+        assert abs(float(np.sum(np.abs(g) ** 2)) - float(G[f"p{p}__energy64"])) <= 1e-5 * float(G[f"p{p}__energy64"])
+
+
+def test_asm_p2048_64_planes_every_plane_vs_oracle():
+    """asm_cols<2048> over 64 planes in two full 32-plane chunks (the kparts split of each chunk's
+    last dispatch round included): every plane vs the fp64 oracle, <= max(1e-4, 1.5 x the oracle's
+    own fp32 error on that plane)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply
+    dev = _dev()
+    rng = np.random.default_rng(21)
+    x = (rng.standard_normal((1, 1, 1024, 1024)) + 1j * rng.standard_normal((1, 1, 1024, 1024))).astype(np.complex64)
+    lam = wavelengths([300])
+    sp = spacing(0.5, 0.5)
+    zs = [float(v) for v in torch.linspace(0.01, 0.25, 64, dtype=torch.float64)]
+    out = asm_apply(torch.from_numpy(x).to(dev), [float(lam[0])], [float(sp[0]), float(sp[1])], zs, 512, 512, True,
+                    1, z_chunk=32).cpu().numpy()
+    xt = torch.from_numpy(x)
+    with torch.no_grad():
+        r64 = orc.asm_forward_planes(xt.to(torch.complex128), lam.double(), sp.double(), zs, 1)
+        r32 = orc.asm_forward_planes(xt, lam, sp, zs, 1)
+        for k, ((_, a), (_, b)) in enumerate(zip(r64, r32)):
+            a = a.numpy()
+            floor = rel_l2(b.numpy(), a)
+            e = rel_l2(out[k], a)
+            assert e <= max(1e-4, 1.5 * floor), (k, zs[k], e, floor)
+
+
+def test_asm_p1024_z_chunk_beyond_workgroup():
+    """P = 1024 runs 64-thread column workgroups; a z_chunk of 100 planes must still find every
+    plane's kept-row bound (the per-z bisection is strided over the workgroup)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_plan_info
+    dev = _dev()
+    rng = np.random.default_rng(22)
+    x = (rng.standard_normal((1, 1, 512, 512)) + 1j * rng.standard_normal((1, 1, 512, 512))).astype(np.complex64)
+    lam = wavelengths([300])
+    sp = spacing(0.5, 0.5)
+    zs = [float(v) for v in torch.linspace(0.01, 0.3, 100, dtype=torch.float64)]
+    lamf, spf = [float(lam[0])], [float(sp[0]), float(sp[1])]
+    assert asm_plan_info(1, 1, 512, 512, 256, 256, True, 1, lamf, spf, zs, 100)[1] == 100
+    out = asm_apply(torch.from_numpy(x).to(dev), lamf, spf, zs, 256, 256, True, 1, z_chunk=100).cpu().numpy()
+    check = [0, 63, 64, 99]
+    xt = torch.from_numpy(x)
+    with torch.no_grad():
+        r64 = orc.asm_forward_planes(xt.to(torch.complex128), lam.double(), sp.double(), [zs[k] for k in check], 1)
+        r32 = orc.asm_forward_planes(xt, lam, sp, [zs[k] for k in check], 1)
+        for k, (_, a), (_, b) in zip(check, r64, r32):
+            a = a.numpy()
+            floor = rel_l2(b.numpy(), a)
+            assert rel_l2(out[k], a) <= max(1e-4, 1.5 * floor), (k, zs[k], floor)
 
 
 @pytest.mark.parametrize("zs,bl,H,W", [([0.02, 0.07, -0.03, 0.15, 0.3], "approx", 100, 100),

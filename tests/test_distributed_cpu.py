@@ -79,3 +79,98 @@ def test_plane_sharding_covers_every_plane_once():
             for r in range(world):
                 seen.extend(shard_planes(n_planes, r, world))
             assert sorted(seen) == list(range(n_planes))
+
+
+class _FakeSystem(torch.nn.Module):
+    """A CPU stand-in for FourFocalSpotsSystem: out = w * x_rank (each rank its own 'noise sample')."""
+
+    def __init__(self, x):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.linspace(-1.0, 1.0, x.numel()).reshape(x.shape))
+        self.x = x
+        self.device = torch.device("cpu")
+
+    def forward(self, frac):
+        import types
+        return types.SimpleNamespace(data=self.w * self.x * (1.0 + frac))
+
+
+def _mse(out, tgt):
+    return ((out - tgt) ** 2).mean()
+
+
+def _trainer_worker(rank, world, port, q):
+    """QATTrainer's eager step runs the same fwd/bwd+pack | all-reduce | unpack+Adam phases the
+    HIP-graph replay is split into; after 3 steps every rank must hold the weights of one Adam
+    trajectory driven by the rank-averaged gradient."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quantizationawarethzdoe_amd.qat import QATTrainer
+        xs = [torch.randn(6, 5, generator=torch.Generator().manual_seed(10 + r)) for r in range(world)]
+        tgt = torch.randn(6, 5, generator=torch.Generator().manual_seed(99))
+        sysm = _FakeSystem(xs[rank])
+        tr = QATTrainer(sysm, tgt, lr=0.05, max_itrs=10, loss_fn=_mse)
+        assert tr.allreduce.world == world
+        for _ in range(3):
+            tr.step()
+        w = sysm.w.detach().clone()
+        allw = [torch.zeros_like(w) for _ in range(world)]
+        dist.all_gather(allw, w)
+        # single-process replay of the same trajectory with the averaged gradient
+        ref = torch.nn.Parameter(torch.linspace(-1.0, 1.0, 30).reshape(6, 5))
+        opt = torch.optim.Adam([ref], lr=0.05)
+        for it in range(3):
+            frac = it / 10
+            opt.zero_grad()
+            loss = sum(_mse(ref * x * (1.0 + frac), tgt) for x in xs) / world
+            loss.backward()
+            opt.step()
+        ok_same = all(torch.equal(a, allw[0]) for a in allw)
+        ok_ref = torch.allclose(w, ref.detach(), atol=1e-6)
+        q.put((rank, ok_same, ok_ref))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trainer_phased_allreduce_gloo_world2():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(a and b for _, a, b in res), res
+
+
+def test_bench_two_ranks_dry_run_gloo():
+    """``bench.py --gpus 2`` without a launcher starts two ranks itself (torch.distributed.run child);
+    the dry run rehearses the orchestration on the CPU over gloo: n_gpus 2, every plane of the
+    128-plane global sweep exactly once, the cfg3 wavelengths and the cfg5 batch likewise."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "3",
+                        "--warmup", "1"], capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["steps"] == 3
+    assert line["planes_covered"] == list(range(128))
+    assert line["wavelengths_covered"] == list(range(32))
+    assert line["samples_covered"] == list(range(256))
+    assert line["value"] == round(2 * 64 * 3 / line["elapsed_max_s"], 2)
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr

@@ -316,3 +316,21 @@ def test_resample_oracle_matches_reference(case):
     gx, = torch.autograd.grad(o, x, grad_outputs=torch.from_numpy(A[f"{k}__gout"]))
     assert rel_l2(o.detach().numpy(), A[f"{k}__out32"]) <= 1e-6
     assert rel_l2(gx.numpy(), A[f"{k}__gx32"]) <= 1e-6
+
+
+def test_asm_oracle_multi_plane_cfg2_matches_reference():
+    """The multi-plane oracle (asm_forward_planes: ft2 once, per-z transfer function) on the cfg2
+    headline workload (4096^2 Gaussian, P = 8192, z = 20 / 120 mm) vs the reference's own fp32
+    output signature (tests/golden/gen_cfg2_check.py)."""
+    from tests.golden_io import GOLDEN
+    G = np.load(f"{GOLDEN}/cfg2_check.npz")
+    lam = torch.from_numpy(G["lam"])
+    d = torch.tensor(float(G["dx"]), dtype=torch.float32)
+    x = orc.gaussian_beam(4096, 4096, d, d, lam, 50e-3, 50e-3).to(torch.complex64)
+    with torch.no_grad():
+        for p, (_, y) in enumerate(orc.asm_forward_planes(x, lam, torch.stack([d, d]), [float(z) for z in G["z"]])):
+            y = y[0, 0].numpy().astype(np.complex128)
+            assert rel_l2(y[::64, ::64], G[f"p{p}__sub32"]) <= 1e-6
+            assert rel_l2(y[2048], G[f"p{p}__row32"]) <= 1e-6
+            e = float(np.sum(np.abs(y) ** 2))
+            assert abs(e - float(G[f"p{p}__energy32"])) <= 1e-6 * e
