@@ -115,8 +115,24 @@ def bench_czt(dev, rank, world, steps=10, warmup=2, dist=None):
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    # per-kernel HIP-event times (separate calls, outside the timed region)
+    from quantizationawarethzdoe_amd import _lib
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    for _ in range(3):
+        czt_apply(x, mine, sp, 0.5, 512, 512, 0.25e-3, 0.25e-3)
+    torch.cuda.synchronize()
+    _lib.timing_enable(False)
+    kern = {}
+    for k in ("czt_tables", "czt_rows", "czt_cols"):
+        ms, n = _lib.timing_read(k)
+        if n:
+            kern[k] = round(ms / n, 4)
+    # SURVEY §8(d) CZT byte model per (b, lambda): 8 (H W + 2 W M1 + M1 M2)
+    model = 8 * (2048 * 2048 + 2 * 2048 * 512 + 512 * 512) * len(mine)
     return {"workload": "cfg3: CZT_prop 2048^2 -> 512^2, 32 wavelengths 220-330 GHz sharded over ranks",
             "value": round(32 * steps / dt, 2), "unit": "propagations/s", "ms_per_call": round(dt / steps * 1e3, 3),
+            "kernel_avg_ms": kern, "hbm_gbs_model": round(model / (dt / steps) / 1e9, 1),
             "scaling": "strong"}
 
 

@@ -18,6 +18,12 @@
 // the last-stage storer.  The chirp tables are generated on the device in DOUBLE precision
 // (the reference's fp32 complex pow is its dominant error), the filter
 // spectra by the same LDS FFT.
+//
+// Forward passes whose output fits half a 1024-point block (M <= 512) and whose input is long
+// (cfg3: m = 2048) run the overlap-add form instead (czt_rows_blk / czt_cols_blk, below): the input
+// split into 512-point blocks, each block's 1024-point spectrum accumulated against a precomputed
+// block filter spectrum, one inverse per line -- 5 transforms of 1024 points per line where the
+// np2 form runs 2 of 4096, on one wavefront per line without workgroup barriers (thz_wfft.hpp).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -25,12 +31,15 @@
 
 #include "thz_common.hpp"
 #include "thz_dev.hpp"
+#include "thz_wfft.hpp"
 
 namespace thz {
 
 struct BluePass {
   int m, M, np2;
   int ntab;        // length of the 1/h sequence actually used: min(mp + 1, Lh)
+  int nb;          // > 0: overlap-add form, nb blocks of CZB_BS inputs (else one np2 transform pair)
+  int nrm;         // inverse-transform length whose 1/n the post table carries (np2 or wf::N)
   double f1, f2;   // frequency range
 };
 
@@ -38,8 +47,9 @@ struct CztArgs {
   int BC, C, H, W, outH, outW;
   float dx, dy, odx, ody, z;
   BluePass pa, pb;   // pass A: W axis (fx, outH); pass B: H axis (fy, outW)
-  int ncbA;          // column blocks of the intermediate V (outH columns)
-  // table offsets (in float2) inside the workspace, per wavelength stride
+  int ncbA;          // blocks of CB columns covering the intermediate V's outH columns (allocation)
+  // table offsets (in float2) inside the workspace, per wavelength stride; ft* holds the np2 filter
+  // spectrum, or for an overlap-add pass the nb block spectra (nb x wf::N)
   size_t preA, postA, ftA, preB, postB, ftB, tabStride;
   float lam[THZ_MAX_WAVELENGTHS];
 };
@@ -85,10 +95,10 @@ __global__ void czt_tables(CztArgs a, float2* __restrict__ ws, int pass) {
     const double ell = l / p.M * (b.D2 - b.D1) + b.D1;
     const double shift = -6.283185307179586476925 * ell * (-p.m / 2.0 + 0.5) / b.Dm;
     const float2 v = cis_d(b.thW * l * l / 2 + shift);
-    const float s = 1.0f / (float)p.np2;
+    const float s = 1.0f / (float)p.nrm;
     post[n] = make_float2(v.x * s, v.y * s);
   }
-  if (n < p.np2) {
+  if (n < p.np2 && !p.nb) {
     if (n < p.ntab) {
       const double jj = n - p.m + 1;
       g[n] = cis_d(-b.thW * jj * jj / 2);
@@ -98,13 +108,14 @@ __global__ void czt_tables(CztArgs a, float2* __restrict__ ws, int pass) {
   }
 }
 
-// Bluestein length 2560 = 8 5 8 8 (cfg3: m + M - 1 = 2559) as a compile-time mixed plan with
-// 320 threads: the radix-8 stages are one butterfly per thread, the first and last radix match
-// so the forward's spectrum stays in registers for the inverse (as the power-of-two path).
-using CztMx = MxPlan<8, 5, 8, 8>;
-constexpr int CZT_MX_T = 320;
-constexpr int CZT_MX_MB = CztMx::N / CztMx::RL / CZT_MX_T;
-static_assert(CZT_MX_MB * CztMx::RL * CZT_MX_T == CztMx::N, "CZT mixed plan: one last-stage block per thread");
+// The intermediate V between the passes: blocked column-major per plane, element (q, h) at
+// ((q / CB) * H + h) * CB + q % CB (q < outH, h < H).  The rows pass stores a row's outputs as whole
+// 128-B lines; the columns pass's 16 waves of a workgroup read one 16-column block, so each line
+// they touch serves all 16.  (Measured against a plain column-major V with the rows pass's outputs
+// transposed through LDS into 32-B column sectors: columns 0.24 -> 0.20 ms, rows 0.55 -> 0.62 ms at
+// cfg3, so the blocked form stays.)
+__device__ __forceinline__ size_t vcol(int q, int h, int H) { return blk(q, h, H); }
+constexpr int VHS = CB;  // stride of consecutive h in a column of V
 
 template <int PN>
 struct CztGeo {
@@ -112,7 +123,7 @@ struct CztGeo {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Pass A: rows (W axis).  in [BC][H][W] -> V blocked [BC][q/16][h][16], q in [0, outH)
+// Pass A: rows (W axis).  in [BC][H][W] -> V [BC][q][h], q in [0, outH)
 // ---------------------------------------------------------------------------------------------
 template <int PN>
 __global__ void __launch_bounds__(1024) czt_rows(const float2* __restrict__ in, float2* __restrict__ V,
@@ -139,20 +150,10 @@ __global__ void __launch_bounds__(1024) czt_rows(const float2* __restrict__ in, 
   };
   auto store_y = [&](int j, float2 v) {
     const int q = j - m;
-    if (q >= 0 && q < M) dst[blk(q, h, a.H)] = cmul(v, post[q]);
+    if (q >= 0 && q < M) dst[vcol(q, h, a.H)] = cmul(v, post[q]);
   };
   int tid = threadIdx.x;
-  if constexpr (PN == CztMx::N) {
-    const auto twr = CztMx::twiddles<CZT_MX_T>(pl.tw, tid);
-    float2 sp[CZT_MX_MB][CztMx::RL];
-    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
-    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    CztMx::run<false, CZT_MX_T>(lds, twr, tid, ld0, sv0);
-    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
-    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    __syncthreads();  // the forward's LDS reads are done before the inverse's first exchange
-    CztMx::run<true, CZT_MX_T>(lds, twr, tid, ld1, sv1);
-  } else if constexpr (PN > 0) {
+  if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = CztGeo<PN>::T;
     constexpr int RL = S::radix(S::NST - 1, false);
@@ -191,7 +192,7 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
   const float lam = a.lam[c];
   const float k = 6.283185307179586f / lam;
   const RsPhase rph = rs_phase(lam, a.z);
-  const float2* col = V + (size_t)bc * a.ncbA * CB * a.H + blk(q, 0, a.H);
+  const float2* col = V + (size_t)bc * a.ncbA * CB * a.H + vcol(q, 0, a.H);
   const float2* pre = ws + a.preB + (size_t)c * a.tabStride;
   const float2* post = ws + a.postB + (size_t)c * a.tabStride;
   const float2* ft = ws + a.ftB + (size_t)c * a.tabStride;
@@ -201,7 +202,7 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
   const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
   const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
   const float cst = ((a.z * a.odx) * a.ody) * lam;
-  auto load_x = [&](int h) { return h < m ? cmul(col[(size_t)h * CB], pre[h]) : make_float2(0.f, 0.f); };
+  auto load_x = [&](int h) { return h < m ? cmul(col[(size_t)h * VHS], pre[h]) : make_float2(0.f, 0.f); };
   auto store_y = [&](int j, float2 v) {
     const int p = j - m;
     if (p >= 0 && p < M) {
@@ -210,17 +211,7 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
     }
   };
   int tid = threadIdx.x;
-  if constexpr (PN == CztMx::N) {
-    const auto twr = CztMx::twiddles<CZT_MX_T>(pl.tw, tid);
-    float2 sp[CZT_MX_MB][CztMx::RL];
-    auto ld0 = [&](int, int, int idx) { return load_x(idx); };
-    auto sv0 = [&](int mm, int r, int, float2 v) { sp[mm][r] = v; };
-    CztMx::run<false, CZT_MX_T>(lds, twr, tid, ld0, sv0);
-    auto ld1 = [&](int mm, int r, int idx) { return cmul(sp[mm][r], ft[idx]); };
-    auto sv1 = [&](int, int, int j, float2 v) { store_y(j, v); };
-    __syncthreads();  // the forward's LDS reads are done before the inverse's first exchange
-    CztMx::run<true, CZT_MX_T>(lds, twr, tid, ld1, sv1);
-  } else if constexpr (PN > 0) {
+  if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = CztGeo<PN>::T;
     constexpr int RL = S::radix(S::NST - 1, false);
@@ -244,6 +235,152 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
     fft_lds<true>(lds, pl, tid, nt);
     for (int j = tid; j < n; j += nt) store_y(j, lds[padx(j)]);
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Overlap-add Bluestein (forward passes with M <= CZB_BS).  Per line the kept outputs are
+//   y[q] = post[q] sum_{w < m} x'[w] g[q + m - w],   q < M,  x' = x pre,  g = 1/h   (:179-225)
+// (a linear correlation: the reference's np2 >= m + M - 1 circular convolution never wraps for the
+// kept rows [m, m + M)).  Split the input into nb blocks of CZB_BS = 512: with
+// g_b[t] = g[t + m - 512 (b + 1)] (zero outside [0, ntab)),
+//   y[q] = post[q] sum_b (x_b (*) g_b)[q + 512],  x_b[u] = x'[512 b + u], u < 512,
+// and since 1 <= q + 512 - u <= 1023 the 1024-point circular convolution equals the linear one:
+//   y[q] = post[q] / 1024 * IFFT_1024( sum_b FFT_1024(x_b) FFT_1024(g_b) )[q + 512].
+// One wavefront per line: nb half-zero forward transforms accumulated in registers against the
+// precomputed block spectra G_b (per wavelength, L2-resident), one inverse keeping its upper half.
+// For cfg3 (m = 2048, M = 512) that is 5 transforms of 1024 points per line instead of 2 of 4096.
+// ---------------------------------------------------------------------------------------------
+constexpr int CZB_BS = wf::N / 2;
+
+constexpr int CZB_W = 4;   // rows pass: lines (waves) per workgroup
+constexpr int CZB_WC = CB;  // columns pass: one 16-column block of V per workgroup
+#ifndef CZB_WPE
+#define CZB_WPE 4
+#endif
+constexpr size_t czb_lds_bytes(int waves) { return wf::TAB * sizeof(float2) + waves * wf::IMG * sizeof(float); }
+
+// g_b[t] for every block b and wavelength (then FFT'd in place by fft_rows_strided)
+__global__ void czt_blk_tables(CztArgs a, float2* __restrict__ ws, int pass) {
+  const int c = blockIdx.z, b = blockIdx.y;
+  const BluePass& p = pass == 0 ? a.pa : a.pb;
+  const BlueD bd = blue_params(p, (double)a.lam[c], (double)a.z, (double)a.dx);
+  float2* g = ws + (pass == 0 ? a.ftA : a.ftB) + ((size_t)c * p.nb + b) * wf::N;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= wf::N) return;
+  const int gi = t + p.m - CZB_BS * (b + 1);
+  if (gi >= 0 && gi < p.ntab) {
+    const double jj = gi - p.m + 1;
+    g[t] = cis_d(-bd.thW * jj * jj / 2);
+  } else {
+    g[t] = make_float2(0.f, 0.f);
+  }
+}
+
+// one overlap-add line on this wave: ld(w0, u) = x'[w0 + u] for block start w0 and u = lane + 64 r
+// (r < 8); st(i, o, v) for output o = lane + 64 i (i < 8; o may exceed M)
+template <class Ld, class St>
+__device__ __forceinline__ void czb_line(float* img, const wf::Tabs& tw, int lane, int nb,
+                                         const float2* __restrict__ G, Ld& ld, St& st) {
+  float2 acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = make_float2(0.f, 0.f);
+  for (int b = 0; b < nb; ++b) {
+    // an opaque copy of the lane id per block: otherwise every twiddle / image address of the
+    // transform is hoisted out of the block loop and held live across it (register spills)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    const float2* Gb = G + (size_t)b * wf::N + ln;
+    auto mac = [&](int i, float2 x) { acc[i] = cadd(acc[i], cmul(x, Gb[64 * (i >> 2) + 256 * (i & 3)])); };
+    const int w0 = CZB_BS * b;
+    auto ldb = [&](int u) { return ld(w0, u); };
+    wf::forward<true>(img, tw, ln, ldb, mac);
+  }
+  auto sv = [&](int q, int j, float2 v) { st(q - 8, j - CZB_BS, v); };
+  wf::inverse<8>(img, tw, lane, acc, sv);
+}
+
+// pass A (rows, W axis): in [BC][H][W] -> V [BC][q][h], q < outH
+// PARTIAL: m is not a multiple of CZB_BS (the last block's loads are bounds-tested)
+template <bool PARTIAL>
+__global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_rows_blk(const float2* __restrict__ in, float2* __restrict__ V,
+                                                           const float2* __restrict__ ws, CztArgs a) {
+  extern __shared__ float2 lds[];
+  const wf::Tabs tw = wf::fill_tables(lds, threadIdx.x, blockDim.x);
+  float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * CZB_W + (threadIdx.x >> 6);
+  if (row >= a.BC * a.H) return;
+  const int bc = row / a.H, h = row - bc * a.H;
+  const int c = bc % a.C;
+  const float lam = a.lam[c];
+  const float k = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, a.z);
+  const float xh = lin(-(float)a.H * a.dx / 2.0f, (float)a.H * a.dx / 2.0f, a.H, h);
+  const float2* src = in + ((size_t)bc * a.H + h) * a.W;
+  const float2* pre = ws + a.preA + (size_t)c * a.tabStride;
+  const float2* post = ws + a.postA + (size_t)c * a.tabStride;
+  const float2* G = ws + a.ftA + (size_t)c * a.pa.nb * wf::N;
+  float2* dst = V + (size_t)bc * a.ncbA * CB * a.H;
+  const int m = a.W, M = a.outH;
+  const float ylo = -(float)a.W * a.dy / 2.0f, yhi = (float)a.W * a.dy / 2.0f;
+  // block-relative pointers: the 8 loads of a block are one address plus immediate offsets
+  auto ld = [&](int w0, int u) {
+    const int w = w0 + u;
+    const float2 F = rs_kernel_fast(xh, lin(ylo, yhi, a.W, w), a.z, k, rph);
+    float2 x = make_float2(0.f, 0.f), pw = make_float2(0.f, 0.f);
+    if (!PARTIAL || w < m) {
+      x = (src + w0)[u];
+      pw = (pre + w0)[u];
+    }
+    return cmul(cmul(x, F), pw);
+  };
+  auto st = [&](int, int q, float2 v) {
+    if (q < M) dst[vcol(q, h, a.H)] = cmul(v, post[q]);
+  };
+  czb_line(img, tw, lane, a.pa.nb, G, ld, st);
+}
+
+// pass B (columns, H axis) of V -> out [BC][outW][outH]: out[p][q] = F0 * U * z dxo dyo lambda
+template <bool PARTIAL>
+__global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_cols_blk(const float2* __restrict__ V, float2* __restrict__ out,
+                                                           const float2* __restrict__ ws, CztArgs a) {
+  extern __shared__ float2 lds[];
+  const wf::Tabs tw = wf::fill_tables(lds, threadIdx.x, blockDim.x);
+  float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int id = blockIdx.x * CZB_WC + (threadIdx.x >> 6);
+  if (id >= a.BC * a.outH) return;
+  const int bc = id / a.outH, q = id - bc * a.outH;
+  const int c = bc % a.C;
+  const float lam = a.lam[c];
+  const float k = 6.283185307179586f / lam;
+  const RsPhase rph = rs_phase(lam, a.z);
+  const float2* col = V + (size_t)bc * a.ncbA * CB * a.H + vcol(q, 0, a.H);
+  const float2* pre = ws + a.preB + (size_t)c * a.tabStride;
+  const float2* post = ws + a.postB + (size_t)c * a.tabStride;
+  const float2* G = ws + a.ftB + (size_t)c * a.pb.nb * wf::N;
+  float2* dst = out + (size_t)bc * a.outW * a.outH + q;
+  const int m = a.H, M = a.outW;
+  const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
+  const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
+  const float cst = ((a.z * a.odx) * a.ody) * lam;
+  auto ld = [&](int h0, int u) {
+    float2 x = make_float2(0.f, 0.f), ph = make_float2(0.f, 0.f);
+    if (!PARTIAL || h0 + u < m) {
+      x = (col + (size_t)h0 * VHS)[(size_t)u * VHS];
+      ph = (pre + h0)[u];
+    }
+    return cmul(x, ph);
+  };
+  auto st = [&](int, int p, float2 v) {
+    if (p < M) {
+      const float2 F0 = rs_kernel_fast(lin(xlo, xhi, a.outH, p), yq, a.z, k, rph);
+      dst[(size_t)p * a.outH] = cscale(cmul(F0, cmul(v, post[p])), cst);
+    }
+  };
+  czb_line(img, tw, lane, a.pb.nb, G, ld, st);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -286,7 +423,7 @@ __device__ __forceinline__ void czt_adj_line(float2* lds, const FftPlan& pl, con
   }
 }
 
-// adjoint of pass B: G [BC][outW][outH] (column q) -> V^ blocked [BC][q/16][h][16]
+// adjoint of pass B: G [BC][outW][outH] (column q) -> V^ [BC][q][h]
 template <int PN>
 __global__ void __launch_bounds__(1024) czt_cols_adj(const float2* __restrict__ G, float2* __restrict__ V,
                                                     const float2* __restrict__ ws, FftPlan pl, CztArgs a) {
@@ -301,7 +438,7 @@ __global__ void __launch_bounds__(1024) czt_cols_adj(const float2* __restrict__ 
   const float2* post = ws + a.postB + (size_t)c * a.tabStride;
   const float2* ft = ws + a.ftB + (size_t)c * a.tabStride;
   const float2* src = G + (size_t)bc * a.outW * a.outH + q;
-  float2* dst = V + (size_t)bc * a.ncbA * CB * a.H + blk(q, 0, a.H);
+  float2* dst = V + (size_t)bc * a.ncbA * CB * a.H + vcol(q, 0, a.H);
   const int m = a.H, M = a.outW, N = pl.n;
   const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
   const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
@@ -314,7 +451,7 @@ __global__ void __launch_bounds__(1024) czt_cols_adj(const float2* __restrict__ 
     return cmul(conjf2(post[p]), cscale(cmul(conjf2(F0), src[(size_t)p * a.outH]), cst));
   };
   auto store_y = [&](int j, float2 v) {
-    if (j < m) dst[(size_t)j * CB] = cmul(conjf2(pre[j]), v);
+    if (j < m) dst[(size_t)j * VHS] = cmul(conjf2(pre[j]), v);
   };
   czt_adj_line<PN>(lds, pl, ft, load_x, store_y);
 }
@@ -342,7 +479,7 @@ __global__ void __launch_bounds__(1024) czt_rows_adj(const float2* __restrict__ 
     int qq = j - m;
     if (qq < 0) qq += N;
     if (qq >= M) return make_float2(0.f, 0.f);
-    return cmul(conjf2(post[qq]), src[blk(qq, h, a.H)]);
+    return cmul(conjf2(post[qq]), src[vcol(qq, h, a.H)]);
   };
   auto store_y = [&](int j, float2 v) {
     if (j < m) {
@@ -362,34 +499,24 @@ static int np2_of(int x) {
   return p;
 }
 
-// THZ_CZT_NICE=1: the shortest 2^a 3^b 5^c length >= mp + 1 instead of the power of two. Any
-// N >= mp + 1 gives the same Bluestein output (the kept rows see g[t] for t in [1, mp] only, so
-// nothing wraps); non-power-of-two lengths take the runtime-plan kernels.
-static int nice_of(int x) {
-  int best = np2_of(x);
-  for (int a = 1; a <= best; a *= 2)
-    for (int b = a; b <= best; b *= 3)
-      for (int c = b; c <= best; c *= 5)
-        if (c >= x && c < best) best = c;
-  return best;
-}
-
-static void make_pass(BluePass* p, int m, int M, double lo, double hi) {
+// Forward passes take the overlap-add form when M fits its half block and it needs fewer
+// 1024-point transforms (nb + 1) than the np2 pair costs in 1024-point equivalents; THZ_CZT_NP2=1
+// forces the np2 form (the adjoint always runs it).
+static void make_pass(BluePass* p, int m, int M, double lo, double hi, bool allow_blk) {
   p->m = m;
   p->M = M;
   const int mp = m + M - 1;
-  static const bool nice = [] { const char* e = getenv("THZ_CZT_NICE"); return e && atoi(e) > 0; }();
-  // THZ_CZT_MX=1 (off by default): a pass whose power of two would be 4096 but fits 2560 takes
-  // the compile-time 2560-point plan of the forward kernels (adjoints run the runtime plan).
-  // Parity-green, but slower at cfg3: czt_rows 1.48 ms against 1.10 ms for the split-exchange
-  // 4096-point path, so the 37.5 % shorter transform does not pay yet.
-  static const bool mx = [] { const char* e = getenv("THZ_CZT_MX"); return e && atoi(e) > 0; }();
-  p->np2 = nice ? nice_of(mp + 1) : np2_of(mp);
-  if (mx && !nice && p->np2 > CztMx::N && mp + 1 <= CztMx::N) p->np2 = CztMx::N;
+  p->np2 = np2_of(mp);
   const int Lh = m + std::max(M - 1, m - 1);  // arange(-m+1, max(M-1, m-1)+1)
   p->ntab = std::min(mp + 1, Lh);
   p->f1 = lo;
   p->f2 = hi;
+  static const bool force_np2 = [] { const char* e = getenv("THZ_CZT_NP2"); return e && atoi(e) > 0; }();
+  const int nb = (m + CZB_BS - 1) / CZB_BS;
+  const double cost_blk = (nb + 1) * (double)wf::N * 10.0;
+  const double cost_np2 = 2.0 * p->np2 * std::log2((double)p->np2);
+  p->nb = (allow_blk && !force_np2 && M <= CZB_BS && cost_blk < cost_np2) ? nb : 0;
+  p->nrm = p->nb ? wf::N : p->np2;
 }
 
 static int czt_validate(const thz_czt_desc* d) {
@@ -425,8 +552,8 @@ static void czt_layout(const thz_czt_desc* d, CztArgs* a, size_t* total) {
   // x_out = linspace(-outH dxo/2, outH dxo/2, outH), y_out likewise (Props/CZT_Prop.py:101-102)
   const double xo = (double)(float)((float)d->outH * d->odx / 2.0f);
   const double yo = (double)(float)((float)d->outW * d->ody / 2.0f);
-  make_pass(&a->pa, d->W, d->outH, -xo, xo);  // second reference Bluestein (:246): fx, outH
-  make_pass(&a->pb, d->H, d->outW, -yo, yo);  // first reference Bluestein (:243): fy, outW
+  make_pass(&a->pa, d->W, d->outH, -xo, xo, !d->adjoint);  // second reference Bluestein (:246): fx, outH
+  make_pass(&a->pb, d->H, d->outW, -yo, yo, !d->adjoint);  // first reference Bluestein (:243): fy, outW
   a->ncbA = (d->outH + CB - 1) / CB;
   size_t off = 0;
   auto take = [&](size_t n) {
@@ -436,13 +563,23 @@ static void czt_layout(const thz_czt_desc* d, CztArgs* a, size_t* total) {
   };
   a->preA = take(a->pa.m);
   a->postA = take(a->pa.M);
-  a->ftA = take(a->pa.np2);
+  a->ftA = a->pa.nb ? 0 : take(a->pa.np2);
   a->preB = take(a->pb.m);
   a->postB = take(a->pb.M);
-  a->ftB = take(a->pb.np2);
+  a->ftB = a->pb.nb ? 0 : take(a->pb.np2);
   a->tabStride = off;
+  // overlap-add block spectra: [C][nb][wf::N] after the per-wavelength tables (one FFT launch)
+  size_t gend = (size_t)a->tabStride * d->C;
+  if (a->pa.nb) {
+    a->ftA = gend;
+    gend += (size_t)d->C * a->pa.nb * wf::N;
+  }
+  if (a->pb.nb) {
+    a->ftB = gend;
+    gend += (size_t)d->C * a->pb.nb * wf::N;
+  }
   for (int c = 0; c < d->C; ++c) a->lam[c] = d->wavelengths[c];
-  const size_t tab = a256((size_t)a->tabStride * d->C * sizeof(float2));
+  const size_t tab = a256(gend * sizeof(float2));
   const size_t vbytes = a256((size_t)a->BC * a->ncbA * CB * d->H * sizeof(float2));
   *total = tab + vbytes;
 }
@@ -464,16 +601,14 @@ static int czt_pow2(int n) {
     default: hipLaunchKernelGGL(KER<0>, __VA_ARGS__); break;                             \
   }
 
-#define THZ_CZT_SWITCH_FWD(n, KER, ...)                                                 \
-  if ((n) == CztMx::N) hipLaunchKernelGGL(KER<CztMx::N>, __VA_ARGS__);                   \
-  else THZ_CZT_SWITCH(n, KER, __VA_ARGS__)
-
 static int czt_lds_attr() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
     const int mx = (int)fft_lds_bytes(FFT_MAX_N);
     const void* ks[] = {
+        (const void*)czt_rows_blk<false>, (const void*)czt_rows_blk<true>,
+        (const void*)czt_cols_blk<false>, (const void*)czt_cols_blk<true>,
         (const void*)czt_rows<0>,     (const void*)czt_rows<1024>, (const void*)czt_rows<2048>,
         (const void*)czt_rows<4096>,  (const void*)czt_rows<8192>, (const void*)czt_rows<16384>,
         (const void*)czt_cols<0>,     (const void*)czt_cols<1024>, (const void*)czt_cols<2048>,
@@ -481,8 +616,7 @@ static int czt_lds_attr() {
         (const void*)czt_rows_adj<0>,  (const void*)czt_rows_adj<1024>, (const void*)czt_rows_adj<2048>,
         (const void*)czt_rows_adj<4096>, (const void*)czt_rows_adj<8192>, (const void*)czt_rows_adj<16384>,
         (const void*)czt_cols_adj<0>,  (const void*)czt_cols_adj<1024>, (const void*)czt_cols_adj<2048>,
-        (const void*)czt_cols_adj<4096>, (const void*)czt_cols_adj<8192>, (const void*)czt_cols_adj<16384>,
-        (const void*)czt_rows<CztMx::N>, (const void*)czt_cols<CztMx::N>};
+        (const void*)czt_cols_adj<4096>, (const void*)czt_cols_adj<8192>, (const void*)czt_cols_adj<16384>};
     for (const void* k : ks) {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       if (e != hipSuccess) err = e;
@@ -493,8 +627,6 @@ static int czt_lds_attr() {
 }
 
 static int threads_pow2_or(int n) { return czt_pow2(n) ? n / pow2_v(n) : fft_threads(n); }
-// forward kernels: the compile-time 2560 plan runs CZT_MX_T threads
-static int threads_fwd(int n) { return n == CztMx::N ? CZT_MX_T : threads_pow2_or(n); }
 
 }  // namespace thz
 
@@ -525,7 +657,7 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   if ((e = get_plan(a.pb.np2, &plB))) return e;
   hipStream_t s = (hipStream_t)stream;
   float2* ws = (float2*)workspace;
-  float2* V = (float2*)((char*)workspace + a256((size_t)a.tabStride * d->C * sizeof(float2)));
+  float2* V = (float2*)((char*)workspace + need - a256((size_t)a.BC * a.ncbA * CB * d->H * sizeof(float2)));
   {
     KernelTimer kt("czt_tables", s);
     const int nA = std::max({a.pa.m, a.pa.M, a.pa.np2}), nB = std::max({a.pb.m, a.pb.M, a.pb.np2});
@@ -535,9 +667,20 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
-  // filter spectra FFT_np2(1/h) in place, one row per wavelength: one launch per axis
-  if ((e = fft_rows_strided(ws + a.ftA, ws + a.ftA, d->C, a.pa.np2, (size_t)a.tabStride, 0, s))) return e;
-  if ((e = fft_rows_strided(ws + a.ftB, ws + a.ftB, d->C, a.pb.np2, (size_t)a.tabStride, 0, s))) return e;
+  // filter spectra in place, one launch per axis: FFT_np2(1/h) (one row per wavelength) or, for an
+  // overlap-add pass, FFT_1024 of each block's g_b (nb rows per wavelength)
+  const BluePass* ps[2] = {&a.pa, &a.pb};
+  const size_t fts[2] = {a.ftA, a.ftB};
+  for (int ax = 0; ax < 2; ++ax) {
+    const BluePass& p = *ps[ax];
+    if (p.nb) {
+      hipLaunchKernelGGL(czt_blk_tables, dim3(wf::N / 256, p.nb, d->C), dim3(256), 0, s, a, ws, ax);
+      THZ_LAUNCH_CHECK();
+      if ((e = fft_rows_strided(ws + fts[ax], ws + fts[ax], d->C * p.nb, wf::N, (size_t)wf::N, 0, s))) return e;
+    } else if ((e = fft_rows_strided(ws + fts[ax], ws + fts[ax], d->C, p.np2, (size_t)a.tabStride, 0, s))) {
+      return e;
+    }
+  }
   if (d->adjoint) {  // G [B, C, outW, outH] -> grad_in [B, C, H, W]: column pass first
     KernelTimer kt("czt_adjoint", s);
     THZ_CZT_SWITCH(a.pb.np2, czt_cols_adj, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
@@ -551,15 +694,25 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   }
   {
     KernelTimer kt("czt_rows", s);
-    THZ_CZT_SWITCH_FWD(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_fwd(a.pa.np2)),
-                   fft_lds_bytes_io(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
+    if (a.pa.nb) {
+      hipLaunchKernelGGL(d->W % CZB_BS ? czt_rows_blk<true> : czt_rows_blk<false>, dim3((a.BC * d->H + CZB_W - 1) / CZB_W), dim3(64 * CZB_W), czb_lds_bytes(CZB_W), s,
+                         (const float2*)in, V, (const float2*)ws, a);
+    } else {
+      THZ_CZT_SWITCH(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
+                     fft_lds_bytes_io(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
+    }
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
   {
     KernelTimer kt("czt_cols", s);
-    THZ_CZT_SWITCH_FWD(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_fwd(a.pb.np2)),
-                   fft_lds_bytes_io(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
+    if (a.pb.nb) {
+      hipLaunchKernelGGL(d->H % CZB_BS ? czt_cols_blk<true> : czt_cols_blk<false>, dim3((a.BC * d->outH + CZB_WC - 1) / CZB_WC), dim3(64 * CZB_WC), czb_lds_bytes(CZB_WC),
+                         s, (const float2*)V, (float2*)out, (const float2*)ws, a);
+    } else {
+      THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
+                     fft_lds_bytes_io(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
+    }
     THZ_LAUNCH_CHECK();
     kt.stop();
   }

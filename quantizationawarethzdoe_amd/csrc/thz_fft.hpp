@@ -178,17 +178,27 @@ __device__ __forceinline__ void dft8(float2* v) {
   v[7] = csub(e3, t3);
 }
 
-template <bool INV>
+// HALF_IN: inputs 8..15 are zero (a zero-padded half transform's first stage), so the first DFT4
+// layer is two-input.
+template <bool INV, bool HALF_IN = false>
 __device__ __forceinline__ void dft16(float2* v) {
   // 16 = 4 x 4: B[r2][q1] = DFT4_{r1}(v[r2 + 4 r1]); B *= w16^(r2 q1); y[q1 + 4 q2] = DFT4_{r2}(B[.][q1])
   float2 b[4][4];
 #pragma unroll
   for (int r2 = 0; r2 < 4; ++r2) {
-    b[r2][0] = v[r2];
-    b[r2][1] = v[r2 + 4];
-    b[r2][2] = v[r2 + 8];
-    b[r2][3] = v[r2 + 12];
-    dft4<INV>(b[r2][0], b[r2][1], b[r2][2], b[r2][3]);
+    if constexpr (HALF_IN) {
+      const float2 a0 = v[r2], a1 = v[r2 + 4];
+      b[r2][0] = cadd(a0, a1);
+      b[r2][2] = csub(a0, a1);
+      b[r2][1] = add_mi<INV>(a0, a1);
+      b[r2][3] = sub_mi<INV>(a0, a1);
+    } else {
+      b[r2][0] = v[r2];
+      b[r2][1] = v[r2 + 4];
+      b[r2][2] = v[r2 + 8];
+      b[r2][3] = v[r2 + 12];
+      dft4<INV>(b[r2][0], b[r2][1], b[r2][2], b[r2][3]);
+    }
   }
   const float s = INV ? 1.f : -1.f;
   // w16^k = cos(2 pi k/16) + s i sin(2 pi k/16), k = r2*q1 in {1,2,3,4,6,9}

@@ -1,0 +1,139 @@
+// Wave-level 1024-point Stockham FFT for gfx950: ONE wavefront (64 lanes x 16 values) owns a
+// transform.  The two data exchanges go through a per-wave LDS image of floats (real parts, then
+// imaginary parts), so a workgroup's waves never wait on each other: no workgroup barriers, only
+// wave-scope ordering of the LDS accesses (a wave's LDS instructions execute in issue order; the
+// fences keep the compiler from reordering them across lanes' data).
+//
+// Used by the overlap-add Bluestein kernels of the chirp-z propagator (thz_czt.hip): per line,
+// several forward transforms of zero-padded half blocks (HALF_IN: inputs 512..1023 are zero) are
+// accumulated in registers against filter spectra and finished by one inverse transform of which
+// only the upper half of the outputs is kept.
+//
+// Forward schedule 16 (L=1), 16 (L=16), 4 (L=256): the result X[j], j = i + 256 q, sits in lane
+// i % 64 as reg[i / 64][q] (i < 256, q < 4).  The inverse starts with radix 4 on exactly those
+// registers, then 16 (L=4), 16 (L=64): output j = lane + 64 q, q < 16.
+// Twiddles: per workgroup in LDS (shared by its waves), exp(-2 pi i t / n) for n = 1024, 256 and 64
+// (TAB entries): each stage reads its own table at k r, which keeps a stage's 16 distinct k of a
+// 32-lane group on distinct banks.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "thz_fft.hpp"
+
+namespace thz {
+namespace wf {
+
+constexpr int N = 1024;
+constexpr int LANES = 64;
+constexpr int IMG = N + N / 32;  // floats per wave image: pad(j) = j + j / 32
+constexpr int TAB = 1024 + 256 + 64;  // float2 twiddle entries per workgroup
+struct Tabs {
+  const float2* t1024;
+  const float2* t256;
+  const float2* t64;
+};
+// image padding: every read pattern of the schedule (x[lane + 64 r] and x[lane + 64 m + 256 r]) is
+// conflict-free on the 32 banks of ds_read_b32 and every write pattern at most 2-way (free on
+// ds_write_b32; MI355X_MICROARCH.md §LDS)
+__device__ __forceinline__ int pad(int j) { return j + (j >> 5); }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// the workgroup's twiddle tables (all threads; barrier before use)
+__device__ __forceinline__ Tabs fill_tables(float2* tab, int tid, int nt) {
+  for (int t = tid; t < TAB; t += nt) {
+    const int n = t < 1024 ? 1024 : (t < 1280 ? 256 : 64);
+    const int e = t < 1024 ? t : (t < 1280 ? t - 1024 : t - 1280);
+    double sn, cs;
+    sincospi(-2.0 * (double)e / (double)n, &sn, &cs);
+    tab[t] = make_float2((float)cs, (float)sn);
+  }
+  return Tabs{tab, tab + 1024, tab + 1280};
+}
+
+// Exchange: this lane's values v[a] go to image position wpos(a); then nx[b] = image[rpos(b)].
+template <int NA, int NB, class WPos, class RPos>
+__device__ __forceinline__ void exchange(float* img, const float2 (&v)[NA], WPos wpos, float2 (&nx)[NB], RPos rpos) {
+#pragma unroll
+  for (int part = 0; part < 2; ++part) {
+#pragma unroll
+    for (int a = 0; a < NA; ++a) img[pad(wpos(a))] = part ? v[a].y : v[a].x;
+    wave_sync();
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const float x = img[pad(rpos(b))];
+      if (part) nx[b].y = x;
+      else nx[b].x = x;
+    }
+    wave_sync();
+  }
+}
+
+// Forward transform of x[idx] = ld(idx) (HALF_IN: ld is only called for idx < N/2, the rest is
+// zero).  Result: out(m * 4 + q, X[lane + 64 m + 256 q]) for m, q < 4.
+template <bool HALF_IN, class Ld, class Out>
+__device__ __forceinline__ void forward(float* img, const Tabs& tw, int lane, Ld& ld, Out& out) {
+  float2 v[16];
+  // stage 0: radix 16, L = 1, butterfly i = lane: inputs x[i + 64 r]
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = (!HALF_IN || r < 8) ? ld(lane + 64 * r) : make_float2(0.f, 0.f);
+  dft16<false, HALF_IN>(v);
+  float2 x1[16];
+  // outputs y[16 i + q] -> stage 1 inputs x[i + 64 r]
+  exchange(img, v, [&](int q) { return 16 * lane + q; }, x1, [&](int r) { return lane + 64 * r; });
+  // stage 1: radix 16, L = 16, k = lane & 15: twiddle w256^(k r)
+  const int k1 = lane & 15;
+#pragma unroll
+  for (int r = 1; r < 16; ++r) x1[r] = cmul(x1[r], tw.t256[k1 * r]);
+  dft16<false>(x1);
+  // outputs y[(i - k) 16 + k + 16 q] -> stage 2 inputs x[i2 + 256 r], i2 = lane + 64 m
+  float2 x2[16];
+  exchange(img, x1, [&](int q) { return (lane - k1) * 16 + k1 + 16 * q; }, x2,
+           [&](int b) { return lane + 64 * (b >> 2) + 256 * (b & 3); });
+  // stage 2: radix 4, L = 256, k = i2: twiddle w1024^(k r)
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int k = lane + 64 * m;
+    float2* q = &x2[4 * m];
+    q[1] = cmul(q[1], tw.t1024[k]);
+    q[2] = cmul(q[2], tw.t1024[2 * k]);
+    q[3] = cmul(q[3], tw.t1024[3 * k]);
+    dft4<false>(q[0], q[1], q[2], q[3]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) out(4 * m + r, q[r]);
+  }
+}
+
+// Inverse (unnormalised) transform of the registers a forward() left: in[m * 4 + q] = X[lane + 64 m
+// + 256 q].  sv(q, j, v) receives output j = lane + 64 q for q in [Q0, 16) only.
+template <int Q0, class Sv>
+__device__ __forceinline__ void inverse(float* img, const Tabs& tw, int lane, float2 (&in)[16], Sv& sv) {
+  // stage 0: radix 4, L = 1, butterflies i = lane + 64 m: inputs x[i + 256 r] = in[4 m + r]
+#pragma unroll
+  for (int m = 0; m < 4; ++m) dft4<true>(in[4 * m], in[4 * m + 1], in[4 * m + 2], in[4 * m + 3]);
+  // outputs y[4 i + q] -> stage 1 inputs x[lane + 64 r]
+  float2 x1[16];
+  exchange(img, in, [&](int a) { return 4 * (lane + 64 * (a >> 2)) + (a & 3); }, x1,
+           [&](int r) { return lane + 64 * r; });
+  // stage 1: radix 16, L = 4, k = lane & 3: conj twiddle w64^(k r)
+  const int k1 = lane & 3;
+#pragma unroll
+  for (int r = 1; r < 16; ++r) x1[r] = cmulc(x1[r], tw.t64[k1 * r]);
+  dft16<true>(x1);
+  // outputs y[(i - k) 16 + k + 4 q] -> stage 2 inputs x[lane + 64 r]
+  float2 x2[16];
+  exchange(img, x1, [&](int q) { return (lane - k1) * 16 + k1 + 4 * q; }, x2, [&](int r) { return lane + 64 * r; });
+  // stage 2: radix 16, L = 64, k = lane: conj twiddle w1024^(k r); outputs y[lane + 64 q]
+#pragma unroll
+  for (int r = 1; r < 16; ++r) x2[r] = cmulc(x2[r], tw.t1024[lane * r]);
+  dft16<true>(x2);
+#pragma unroll
+  for (int q = Q0; q < 16; ++q) sv(q, lane + 64 * q, x2[q]);
+}
+
+}  // namespace wf
+}  // namespace thz
