@@ -131,8 +131,7 @@ class ASM_prop(nn.Module):
         wl = field.wavelengths_host
         sp = field.spacing_host
         self._zc_diagnostic(H + 2 * ph, sp[0], wl, zs[0])
-        cdt = data.dtype
-        x = data if cdt == torch.complex64 else data.to(torch.complex64)
+        x = _prop.kernel_dtype(data, "ASM_prop", field.wavelengths)
         try:
             out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=(not self.do_padding) or self.do_unpad_after_pad,
                                       bandlimit=bl)
@@ -144,7 +143,7 @@ class ASM_prop(nn.Module):
                   "should be at most 1/2 the size of the input field after padding.")
             print("##################################################")
             raise err
-        return out if cdt == torch.complex64 else out.to(cdt)
+        return out
 
     def forward(self, field: ElectricField) -> ElectricField:
         """pad -> ft2 -> x H -> ift2 -> crop (Props/ASM_Prop.py:314-378), on the MI355X kernels."""

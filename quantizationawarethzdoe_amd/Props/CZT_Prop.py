@@ -56,12 +56,9 @@ class CZT_prop(nn.Module):
         odx = sp[0] if outputPixel_dx is None else _f(outputPixel_dx)
         ody = sp[1] if outputPixel_dy is None else _f(outputPixel_dy)
         data = field.data
-        cdt = data.dtype
-        x = data if cdt == torch.complex64 else data.to(torch.complex64)
+        x = _prop.kernel_dtype(data, "CZT_prop", field.wavelengths)
         out = _CztFunction.apply(x, tuple(field.wavelengths_host), tuple(sp), self._zh, outputHeight, outputWidth,
                                  odx, ody)
-        if cdt != torch.complex64:
-            out = out.to(cdt)
         sp_out = [outputPixel_dx if outputPixel_dx is not None else field.spacing[0],
                   outputPixel_dy if outputPixel_dy is not None else field.spacing[1]]
         if all(torch.is_tensor(v) for v in sp_out):

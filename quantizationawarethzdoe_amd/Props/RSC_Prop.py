@@ -87,11 +87,8 @@ class RSC_prop(nn.Module):
         if self.check_Zc:
             self.check_RS_minimum_z(1, sp[0], sp[1], min(wl), Ph=H + 2 * (H // 2))
             self.check_Zc = False
-        cdt = data.dtype
-        x = data if cdt == torch.complex64 else data.to(torch.complex64)
+        x = _prop.kernel_dtype(data, "RSC_prop", field.wavelengths)
         out = _RscFunction.apply(x, tuple(wl), tuple(sp), self._zh, self._vectorial)
-        if cdt != torch.complex64:
-            out = out.to(cdt)
         Eout = ElectricField(data=out, wavelengths=field.wavelengths, spacing=field.spacing, device=field.device)
         return Eout._adopt_host(field)
 

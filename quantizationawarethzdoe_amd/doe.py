@@ -67,8 +67,8 @@ class _Modulate(torch.autograd.Function):
 
 def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None):
     """Differentiable DOE modulation on the HIP kernel; returns (out, noisy full-size height)."""
-    if field.dtype != torch.complex64:
-        raise TypeError(f"DOE kernels compute in complex64; got {field.dtype}")
+    from quantizationawarethzdoe_amd.propagation import kernel_dtype
+    field = kernel_dtype(field, "DOE modulate")
     if tolerance is not None and noise is None:
         noise = torch.rand_like(height)
     if noise is not None:

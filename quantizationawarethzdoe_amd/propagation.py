@@ -22,6 +22,26 @@ def _require_device(t: torch.Tensor, what: str):
                            "this framework has no CPU compute path")
 
 
+def kernel_dtype(data: torch.Tensor, who: str, wavelengths=None) -> torch.Tensor:
+    """The field as the kernels' complex64.  The reference computes in the field's own precision: a
+    float64 wavelength tensor or complex128 data runs it in fp64 and returns complex128
+    (DataType/ElectricField.py:85-90; its smoke script test_czt.py:12 does so).  The MI355X kernels
+    are fp32 only, and narrowing a complex128 field without a word would hand back fp32 accuracy
+    under an fp64 dtype, so double precision is refused with TypeError (as the DOE modulation
+    does); real float32 data is promoted to complex64 as torch's complex products promote it."""
+    if torch.is_tensor(wavelengths) and wavelengths.dtype == torch.float64:
+        raise TypeError(f"{who}: float64 wavelengths make the reference compute in fp64 and return complex128 "
+                        f"(DataType/ElectricField.py:85-90); the MI355X kernels compute in fp32 -- pass float32 "
+                        f"wavelengths (a float / list, or a float32 tensor).")
+    if data.dtype == torch.complex64:
+        return data
+    if data.dtype in (torch.float32, torch.float16, torch.bfloat16):
+        return data.to(torch.complex64)
+    raise TypeError(f"{who}: the MI355X kernels compute in complex64 (fp32); got {data.dtype}. The reference "
+                    f"runs double-precision fields in fp64 (DataType/ElectricField.py:85-90); this build does not "
+                    f"-- cast the field to complex64 (e.g. ElectricField(data.to(torch.complex64), ...)).")
+
+
 def _stream_handle():
     return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
 

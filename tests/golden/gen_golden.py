@@ -242,6 +242,47 @@ def gen_czt_rsc(manifest):
     np.savez_compressed(os.path.join(HERE, "rsc_golden.npz"), **arrays)
 
 
+VRS_CASES = [
+    dict(name="vrs40x48", B=3, f=[C0 / 1e-3 / 1e9], H=40, W=48, dx=1.0, dy=1.2, z=0.25),
+    dict(name="vrs32_2wl", B=3, f=[250, 300], H=32, W=32, dx=1.0, dy=1.0, z=0.2),
+]
+
+
+def run_vrs(case, data_np, f64, grad_np=None):
+    """VRS_prop (Props/RSC_Prop.py:218-321): B = 3 input (Ex, Ey, Ez); Ez is recomputed from Ex, Ey."""
+    wl = [C0 / (g * 1e9) for g in case["f"]]
+    dt = torch.float64 if f64 else torch.float32
+    with default_dtype(dt):
+        field = make_field(data_np, wl_arg(wl), [case["dx"] * MM, case["dy"] * MM], f64)
+        prop = ref.RSC.VRS_prop(z_distance=case["z"], device="cpu")
+        if grad_np is None:
+            out, txt = quiet(prop.forward, field)
+            return out.data.detach().numpy(), txt, None
+        field._data = field._data.clone().requires_grad_(True)
+        out, txt = quiet(prop.forward, field)
+        g = torch.from_numpy(grad_np.astype(np.complex128 if f64 else np.complex64))
+        (gin,) = torch.autograd.grad(out.data, field._data, grad_outputs=g)
+        return out.data.detach().numpy(), txt, gin.numpy()
+
+
+def gen_vrs(manifest):
+    arrays = {}
+    manifest["vrs"] = []
+    for i, case in enumerate(VRS_CASES):
+        shape = (case["B"], len(case["f"]), case["H"], case["W"])
+        x = rand_field(shape, 3500 + i)
+        o32, txt, _ = run_vrs(case, x, False)
+        g = rand_field(o32.shape, 3600 + i)
+        o64, _, gi64 = run_vrs(case, x, True, g)
+        k = case["name"]
+        arrays.update({f"{k}__in": x, f"{k}__out32": o32.astype(np.complex64), f"{k}__out64": o64.astype(np.complex128),
+                       f"{k}__gout": g, f"{k}__gin64": gi64.astype(np.complex128)})
+        rel = np.linalg.norm(o32 - o64) / np.linalg.norm(o64)
+        manifest["vrs"].append(dict(case, stdout=txt.strip(), rel32vs64=float(rel)))
+        print(f"vrs {k}: out {o32.shape} rel {rel:.2e}")
+    np.savez_compressed(os.path.join(HERE, "vrs_golden.npz"), **arrays)
+
+
 # ----------------------------------------------------------------------------------------------
 # DOE modulation + quantizers (Components/QuantizedDOE.py)
 # ----------------------------------------------------------------------------------------------
@@ -614,6 +655,32 @@ def gen_addons(manifest):
     print("addons", len(manifest["addons"]))
 
 
+def gen_save(manifest):
+    """The byte image of a DOE layer's .save() (Components/QuantizedDOE.py:253-267): np.save of
+    {'thickness': cropped height map, 'dxy': doe_dxy}.  The reference layer is built on the CPU, its
+    height map set to a seeded 40 x 40 float32 map and saved with crop (30, 24)."""
+    import glob
+    import tempfile
+    torch.manual_seed(7)
+    dp = {'doe_size': [40, 40], 'doe_dxy': 1 * MM, 'doe_level': 4, 'look_up_table': None, 'num_unit': None,
+          'height_constraint_max': 1 * MM, 'tolerance': 10e-6, 'material': [2.66, 0.03]}
+    layer = ref.DOE.FullPrecisionDOELayer(dp, device="cpu")
+    layer.height_map = torch.from_numpy(np.random.default_rng(41).random((1, 1, 40, 40)).astype(np.float32) * 1e-3)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as d:
+        os.chdir(d)
+        try:
+            layer.save((30, 24))
+            (f,) = glob.glob("height_map_*.npy")
+            data = open(f, "rb").read()
+        finally:
+            os.chdir(cwd)
+    with open(os.path.join(HERE, "save_ref.bin"), "wb") as fh:
+        fh.write(data)
+    manifest["save"] = dict(doe_params=dp, seed=41, shape=[1, 1, 40, 40], crop=[30, 24], nbytes=len(data))
+    print("save", len(data), "bytes")
+
+
 def main():
     path = os.path.join(HERE, "manifest.json")
     if "--only" in sys.argv:
@@ -621,19 +688,21 @@ def main():
         with open(path) as fh:
             manifest = json.load(fh)
         {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat, "donn": gen_donn,
-         "addons": gen_addons}[which](manifest)
+         "addons": gen_addons, "vrs": gen_vrs, "save": gen_save}[which](manifest)
     else:
         manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
                     "asm": [], "czt": [], "rsc": [], "doe": []}
         gen_asm(manifest)
         gen_asm_cfg1(manifest)
         gen_czt_rsc(manifest)
+        gen_vrs(manifest)
         gen_doe(manifest)
         gen_doe_layers(manifest)
         gen_optics(manifest)
         gen_qat(manifest)
         gen_donn(manifest)
         gen_addons(manifest)
+        gen_save(manifest)
     with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1, default=float)
 
