@@ -123,7 +123,7 @@ def test_vczt_alias_propagates_each_component(case):
     field = ElectricField(vec.to(dev), wavelengths=wl if len(wl) > 1 else wl[0],
                           spacing=[case["dx"] * 1e-3, case["dy"] * 1e-3], device=dev)
     prop = VCZT_prop(z_distance=case["z"], device=dev)
-    assert abs(float(prop.z) - case["z"]) < 1e-12
+    assert abs(float(prop.z) - case["z"]) <= 1e-7 * case["z"]  # stored as a float32 tensor, as the reference does
     out = prop(field, outputHeight=case["oH"], outputWidth=case["oW"], outputPixel_dx=case["odx"] * 1e-3,
                outputPixel_dy=case["ody"] * 1e-3).data.cpu().numpy()
     y = A[f"{k}__out64"]
