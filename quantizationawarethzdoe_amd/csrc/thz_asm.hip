@@ -142,13 +142,8 @@ struct Geo {
 // Compile-time mixed-radix sizes (MxPlan, one 64-thread workgroup per transform): the P = 300
 // grid of the cfg4 / cfg5 layers.  Other non-power-of-two sizes run the runtime plan.
 constexpr int MX_T = 64;
-#ifndef THZ_MX
-#define THZ_MX 1
-#endif
-#ifndef THZ_MX_WPE
-#define THZ_MX_WPE 8
-#endif
-__host__ __device__ constexpr bool is_mx(int n) { return THZ_MX && n == Mx300::N; }
+constexpr int MX_WPE = 8;  // waves per SIMD of the mixed-radix column pass (46 VGPRs, no scratch)
+__host__ __device__ constexpr bool is_mx(int n) { return n == Mx300::N; }
 
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
   const int c = freq_index(j, P) + J;
@@ -224,11 +219,8 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // ---------------------------------------------------------------------------------------------
 // K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
 // ---------------------------------------------------------------------------------------------
-#ifndef THZ_K2_WPE
-#define THZ_K2_WPE 1
-#endif
 template <int PN>
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(THZ_K2_WPE))) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+__global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   extern __shared__ float2 lds[];
   // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
@@ -441,7 +433,7 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
 // the runtime plan's numerics at the output (1 / (Ph Pw) is not a power of two here, so the
 // scale is applied to each output element as asm_cols<0> does).
 template <class MP>
-__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_MX_WPE))) asm_cols_mx(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                     AsmArgs a) {
   constexpr int PN = MP::N, RL = MP::RL, NBL = PN / RL, MBL = (NBL + MX_T - 1) / MX_T;
   static_assert(MP::R0 == RL, "the inverse must start where the forward ends");
@@ -515,82 +507,6 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_M
   }
 }
 
-// K2 for P = 300 as 20 x 15: forward FP = <20, 15>, inverse IP = <15, 20> (the inverse's first
-// radix is the forward's last, so the spectrum stays in registers), each transform on a group of
-// TC = 20 lanes with its own LDS image, NCW = 3 columns per 64-lane wave (lanes 60-63 run a
-// discarded copy).  Two Stockham stages (one LDS exchange) per transform and 45-60 busy lanes per
-// stage, against four stages of 60, 100, 75 and 60 butterflies on 64 lanes for Mx300.
-#ifndef THZ_MX3
-#define THZ_MX3 0  // measured slower; kept as an experiment switch
-#endif
-#ifndef THZ_MX3_WPE
-#define THZ_MX3_WPE 1
-#endif
-using Mx300f = MxPlan<20, 15>;
-using Mx300i = MxPlan<15, 20>;
-constexpr int MX3_TC = 20, MX3_NCW = 3;
-__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(THZ_MX3_WPE))) asm_cols_mx3(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
-                                                     AsmArgs a) {
-  constexpr int PN = Mx300f::N, RL = Mx300f::RL, NBL = PN / RL;
-  static_assert(Mx300i::R0 == RL && NBL == MX3_TC, "the inverse must start where the forward ends");
-  extern __shared__ float2 lds_all[];
-  const int lane = threadIdx.x;
-  const int cw = min(lane / MX3_TC, MX3_NCW);
-  const int tid = lane - cw * MX3_TC;
-  float2* lds = lds_all + cw * lds_floats2(PN);
-  // the forward's spectrum, in a second image (each lane reads back only what it wrote)
-  float2* spl = lds_all + (MX3_NCW + 1) * lds_floats2(PN) + cw * PN;
-  const int id = xcd_chunk(blockIdx.x, gridDim.x) * MX3_NCW + cw;
-  const bool live = cw < MX3_NCW && id < a.BC * a.ncols;
-  const int idc = live ? id : 0;
-  const int bc = idc / a.ncols, c = idc - bc * a.ncols;
-  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
-  auto ld0 = [&](int, int, int idx) {
-    const int s = idx - a.in_r0;
-    return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
-  };
-  auto sv0 = [&](int, int, int idx, float2 v) { spl[idx] = v; };
-  {
-    const auto twf = Mx300f::twiddles<MX3_TC>(ph.tw, tid);
-    Mx300f::run<false, MX3_TC>(lds, twf, tid, ld0, sv0);
-  }
-  const auto twi = Mx300i::twiddles<MX3_TC>(ph.tw, tid);
-  if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
-    const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
-    auto ld1 = [&](int m, int r, int idx) {
-      const float2 t = tcol[idx];
-      return cmul(spl[idx], a.adjoint ? make_float2(t.x, -t.y) : t);
-    };
-    float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
-    auto sv1 = [&](int, int, int j, float2 v) {
-      const int r = j - a.out_r0;
-      if (live && r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
-    };
-    Mx300i::run<true, MX3_TC>(lds, twi, tid, ld1, sv1);
-    return;
-  }
-  const size_t tc = (size_t)(bc % a.C) * a.ncols + c;
-  const int* mzc = a.mzt + tc * a.nz;
-  const float* sqc = a.sqt + tc * PN;
-  for (int zz = 0; zz < a.nz; ++zz) {
-    const float z = a.zv[a.zoff + zz];
-    const int M = mzc[zz];
-    auto ld1 = [&](int m, int r, int idx) {
-      const int mx = freq_index(idx, PN);
-      if (mx > M || -mx > M) return make_float2(0.f, 0.f);
-      float sn, cs;
-      sincos_hw(tf_mul(z, sqc[idx]), &sn, &cs);
-      return cmul(spl[idx], make_float2(cs, a.adjoint ? -sn : sn));
-    };
-    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
-    auto sv1 = [&](int, int, int j, float2 v) {
-      const int r = j - a.out_r0;
-      if (live && (unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
-    };
-    Mx300i::run<true, MX3_TC>(lds, twi, tid, ld1, sv1);
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
 // K3: per output row: gather band from U, IFFT(Pw), crop -> out[z][bc][r][w]
 // ---------------------------------------------------------------------------------------------
@@ -620,25 +536,6 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
     // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
     // frequencies), a multiple of CBU: the blocked address is then base(c0) + delta_q*Hout,
     // one add per element instead of the full blk_u() per element.
-    if constexpr (FFT_ROWS == 3 && Pow2Sched<PN>::PAIR) {
-      // lane-pair radix-32 first stage: lane e of butterfly i reads j = i + (16 e + q) PN/32, band
-      // column c0 + q PN/32 with c0 = i + J - e PN/2 (the upper half holds the negative
-      // frequencies); floor division by CBU keeps the blocked address affine in q for c0 < 0
-      constexpr int LP = PN / 32;
-      static_assert(CBU == 4 && LP % CBU == 0, "pair-first gather offsets");
-      const int c0 = pair_i(tid) + a.J - ((tid >> 5) & 1) * (PN / 2);
-      const float2* base = src + ((long)(c0 >> 2) * a.Hout + r) * CBU + (c0 & (CBU - 1));
-      auto ld = [&](int, int q, int) {
-        if ((unsigned)(c0 + q * LP) >= (unsigned)a.ncols) return make_float2(0.f, 0.f);
-        return base[(long)(q * LP) * a.Hout];
-      };
-      auto sv = [&](int, int, int j, float2 v) {
-        const int w = j - a.out_c0;
-        if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
-      };
-      fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
-      return;
-    }
     constexpr int NB0 = PN / pow2_v(PN);  // first stage: radix pow2_v, L = 1
     static_assert(NB0 % CBU == 0, "band offsets must be whole U blocks");
     static_assert(Geo<PN>::T == NB0, "one first-stage butterfly per thread: i = tid");
@@ -653,7 +550,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
       const int w = j - a.out_c0;
       if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
     };
-    fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS == 3 ? 0 : FFT_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);
@@ -983,13 +880,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
           THZ_LAUNCH_CHECK();
         }
       }
-      if (THZ_MX3 && mx_kind(g.Ph) == Mx300::N) {
-        const int ngrp = (g.BC * g.ncols + MX3_NCW - 1) / MX3_NCW;
-        a.kfull = ngrp;
-        a.kparts = 1;
-        const size_t lds3 = (size_t)(MX3_NCW + 1) * (lds_floats2(g.Ph) + g.Ph) * sizeof(float2);
-        hipLaunchKernelGGL(asm_cols_mx3, dim3(ngrp), dim3(MX_T), lds3, s, (const float2*)T, U, ph, a);
-      } else if (mx_kind(g.Ph) == Mx300::N) {
+      if (mx_kind(g.Ph) == Mx300::N) {
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);

@@ -58,7 +58,7 @@ inline size_t fft_lds_bytes(int n) { return (size_t)(lds_floats2(n) + tw_lds_cou
 // per element) for the compile-time power-of-two sizes, the complex image for runtime plans
 inline size_t fft_lds_bytes_io(int n) {
   const bool pow2 = n >= 1024 && n <= 16384 && (n & (n - 1)) == 0;
-  if (THZ_SPLIT && pow2) return (size_t)(lds_split_f2(n) + tw_lds_count(n)) * sizeof(float2);
+  if (pow2) return (size_t)(lds_split_f2(n) + tw_lds_count(n)) * sizeof(float2);
   return fft_lds_bytes(n);
 }
 

@@ -500,8 +500,8 @@ static int np2_of(int x) {
 }
 
 // Forward passes take the overlap-add form when M fits its half block and it needs fewer
-// 1024-point transforms (nb + 1) than the np2 pair costs in 1024-point equivalents; THZ_CZT_NP2=1
-// forces the np2 form (the adjoint always runs it).
+// 1024-point transforms (nb + 1) than the np2 pair costs in 1024-point equivalents (the adjoint
+// always runs the np2 form).
 static void make_pass(BluePass* p, int m, int M, double lo, double hi, bool allow_blk) {
   p->m = m;
   p->M = M;
@@ -511,11 +511,10 @@ static void make_pass(BluePass* p, int m, int M, double lo, double hi, bool allo
   p->ntab = std::min(mp + 1, Lh);
   p->f1 = lo;
   p->f2 = hi;
-  static const bool force_np2 = [] { const char* e = getenv("THZ_CZT_NP2"); return e && atoi(e) > 0; }();
   const int nb = (m + CZB_BS - 1) / CZB_BS;
   const double cost_blk = (nb + 1) * (double)wf::N * 10.0;
   const double cost_np2 = 2.0 * p->np2 * std::log2((double)p->np2);
-  p->nb = (allow_blk && !force_np2 && M <= CZB_BS && cost_blk < cost_np2) ? nb : 0;
+  p->nb = (allow_blk && M <= CZB_BS && cost_blk < cost_np2) ? nb : 0;
   p->nrm = p->nb ? wf::N : p->np2;
 }
 

@@ -31,14 +31,8 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 // (the L2 writes back partially dirty sectors at a cost: measured K2 1.93 ms at 16 columns,
 // 1.69 at 8, 1.39 at 4, 1.33 unblocked), while the row pass still gathers whole sectors
 // (K3 1.05 ms at 16, 1.22 at 4, 2.59 unblocked).  cfg2 sum per z-chunk is lowest at 4.
-#ifndef THZ_CB
-#define THZ_CB 16
-#endif
-#ifndef THZ_CBU
-#define THZ_CBU 4
-#endif
-constexpr int CB = THZ_CB;
-constexpr int CBU = THZ_CBU;
+constexpr int CB = 16;
+constexpr int CBU = 4;
 __device__ __forceinline__ size_t blk(int c, int row, int rows) {
   return ((size_t)(c / CB) * rows + row) * CB + (c % CB);
 }

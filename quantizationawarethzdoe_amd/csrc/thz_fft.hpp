@@ -24,23 +24,15 @@
 namespace thz {
 
 constexpr int FFT_MAX_STAGES = 24;
-#ifndef THZ_SPLIT
-#define THZ_SPLIT 1
-#endif
 // Split-exchange row kernels of 8192 / 16384 points: the LDS image allows 8 waves / SIMD, so
 // hold them to 64 VGPRs (the smaller sizes are LDS-limited below 8 and would only spill).
-#ifndef THZ_ROW_WPE
-#define THZ_ROW_WPE 8
-#endif
-__host__ __device__ constexpr int row_waves_per_eu(int n) { return THZ_SPLIT && n >= 8192 ? THZ_ROW_WPE : 1; }
+__host__ __device__ constexpr int row_waves_per_eu(int n) { return n >= 8192 ? 8 : 1; }
 #define THZ_ROW_ATTR __attribute__((amdgpu_waves_per_eu(row_waves_per_eu(PN))))
 constexpr int FFT_MAXV = 16;  // complex values held per thread per stage (N <= 16 * threads)
-#ifndef THZ_PV
-#define THZ_PV 16
-#endif
-// Power-of-two path: values (= largest radix) per thread, THZ_PV where N / THZ_PV threads fit
-// one workgroup (1024), else 16.  T = N / pow2_v(N) threads per transform.
-__host__ __device__ constexpr int pow2_v(int n) { return n / THZ_PV <= 1024 ? THZ_PV : 16; }
+// Power-of-two path: 16 values (= the largest radix) per thread, T = N / 16 threads per transform.
+// (8 values per thread measured slower on cfg2: one more LDS exchange costs more than the doubled
+// occupancy hides)
+__host__ __device__ constexpr int pow2_v(int) { return 16; }
 constexpr int pow2_log(int v) { return v <= 1 ? 0 : 1 + pow2_log(v >> 1); }
 
 struct FftPlan {
@@ -53,53 +45,8 @@ struct FftPlan {
 __device__ __forceinline__ int padx(int a) { return a + (a >> 4); }
 __host__ __device__ constexpr int lds_floats2(int n) { return n + (n >> 4) + 1; }
 
-// Complex arithmetic.  THZ_PK=1 builds it on packed fp32: a complex value is one 64-bit VGPR
-// pair and every operation is one v_pk_{add,mul,fma}_f32, with the swaps and sign flips of a
-// complex product / a multiply by -+i on the op_sel / neg modifiers (inline asm: the compiler
-// would materialise them as moves).  That halves the VALU instruction count of a butterfly but
-// not its issue cycles (a packed op occupies the SIMD-32 for both halves), and the aligned
-// register pairs push the column pass into spills: measured on cfg2, K3 -1 %, K2 +10 %.  The
-// scalar form is the default.
-#ifndef THZ_PK
-#define THZ_PK 0
-#endif
-typedef float pf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ pf2 pk(float2 a) { return (pf2){a.x, a.y}; }
-__device__ __forceinline__ float2 upk(pf2 a) { return make_float2(a.x, a.y); }
-
-#if THZ_PK
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return upk(pk(a) + pk(b)); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return upk(pk(a) - pk(b)); }
-// (a.x b.x - a.y b.y, a.x b.y + a.y b.x): t = a.xx * b, then fma((a.y, a.y), (b.y, b.x), t) with
-// the low product negated
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  const pf2 pa = pk(a), pb = pk(b);
-  const pf2 t = pa.xx * pb;
-  pf2 r;
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]"
-      : "=v"(r) : "v"(pa), "v"(pb), "v"(t));
-  return upk(r);
-}
-// a * conj(b) = (a.x b.x + a.y b.y, a.y b.x - a.x b.y)
-__device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
-  pf2 t, r;
-  asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(t) : "v"(pk(a)), "v"(pk(b)));
-  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(b)), "v"(t));
-  return upk(r);
-}
-__device__ __forceinline__ float2 cscale(float2 a, float s) { return upk(pk(a) * s); }
-// a + (-i) d = (a.x + d.y, a.y - d.x)   and   a - (-i) d = (a.x - d.y, a.y + d.x)
-__device__ __forceinline__ float2 add_mfwd(float2 a, float2 d) {
-  pf2 r;
-  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
-  return upk(r);
-}
-__device__ __forceinline__ float2 sub_mfwd(float2 a, float2 d) {
-  pf2 r;
-  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(pk(a)), "v"(pk(d)));
-  return upk(r);
-}
-#else
+// Complex arithmetic on scalar fp32 (a packed v_pk_* form measured no faster: a packed op holds the
+// SIMD for both halves, and its aligned register pairs push the column pass into spills).
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
@@ -111,7 +58,6 @@ __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 __device__ __forceinline__ float2 add_mfwd(float2 a, float2 d) { return make_float2(a.x + d.y, a.y - d.x); }
 __device__ __forceinline__ float2 sub_mfwd(float2 a, float2 d) { return make_float2(a.x - d.y, a.y + d.x); }
-#endif
 // a * w (forward) or a * conj(w) (inverse): twiddles are stored and combined unconjugated
 template <bool INV>
 __device__ __forceinline__ float2 cmul_tw(float2 a, float2 w) { return INV ? cmulc(a, w) : cmul(a, w); }
@@ -283,70 +229,6 @@ __device__ __forceinline__ void dft7(float2* v) {
   v[4] = make_float2(m3.x + p3.y, m3.y - p3.x);
 }
 
-// Composite in-register DFT of N = R1 R2 points (natural order in and out), Cooley-Tukey:
-// R1 DFTs of R2 points over n2 of v[n1 + R1 n2], twiddles W_N^(n1 k2) folded to compile-time
-// constants, then R2 DFTs of R1 points -> v[k2 + R2 k1].
-constexpr double ce_pi = 3.14159265358979323846;
-constexpr double ce_sin_red(double x) {  // |x| <= pi
-  double t = x, s = x;
-  for (int k = 1; k < 14; ++k) {
-    t *= -x * x / ((2.0 * k) * (2.0 * k + 1.0));
-    s += t;
-  }
-  return s;
-}
-constexpr double ce_cos_red(double x) {
-  double t = 1.0, s = 1.0;
-  for (int k = 1; k < 14; ++k) {
-    t *= -x * x / ((2.0 * k - 1.0) * (2.0 * k));
-    s += t;
-  }
-  return s;
-}
-// exp(-2 pi i e / N) components, angle reduced to [-pi, pi]
-constexpr double ce_ang(int e, int n) {
-  const int r = e % n;
-  return 2.0 * ce_pi * (double)(2 * r > n ? r - n : r) / (double)n;
-}
-template <int N, int E>
-struct CeTw {
-  static constexpr float c = (float)ce_cos_red(ce_ang(E, N));
-  static constexpr float s = (float)-ce_sin_red(ce_ang(E, N));
-};
-
-template <int R, bool INV>
-__device__ __forceinline__ void dftR(float2* v);
-
-template <int R1, int R2, bool INV, int I>
-__device__ __forceinline__ void ct_tw_one(float2 (&t)[R1][R2]) {
-  constexpr int n1 = I / R2, k2 = I % R2, e = (n1 * k2) % (R1 * R2);
-  if constexpr (e != 0) t[n1][k2] = cmul_tw<INV>(t[n1][k2], make_float2(CeTw<R1 * R2, e>::c, CeTw<R1 * R2, e>::s));
-}
-template <int R1, int R2, bool INV, int... I>
-__device__ __forceinline__ void ct_tw_all(float2 (&t)[R1][R2], std::integer_sequence<int, I...>) {
-  (ct_tw_one<R1, R2, INV, I>(t), ...);
-}
-template <int R1, int R2, bool INV>
-__device__ __forceinline__ void dft_ct(float2* v) {
-  float2 t[R1][R2];
-#pragma unroll
-  for (int n1 = 0; n1 < R1; ++n1) {
-#pragma unroll
-    for (int n2 = 0; n2 < R2; ++n2) t[n1][n2] = v[n1 + R1 * n2];
-    dftR<R2, INV>(t[n1]);
-  }
-  ct_tw_all<R1, R2, INV>(t, std::make_integer_sequence<int, R1 * R2>{});
-#pragma unroll
-  for (int k2 = 0; k2 < R2; ++k2) {
-    float2 u[R1];
-#pragma unroll
-    for (int n1 = 0; n1 < R1; ++n1) u[n1] = t[n1][k2];
-    dftR<R1, INV>(u);
-#pragma unroll
-    for (int k1 = 0; k1 < R1; ++k1) v[k2 + R2 * k1] = u[k1];
-  }
-}
-
 template <int R, bool INV>
 __device__ __forceinline__ void dftR(float2* v) {
   if constexpr (R == 2) dft2<INV>(v[0], v[1]);
@@ -356,9 +238,6 @@ __device__ __forceinline__ void dftR(float2* v) {
   else if constexpr (R == 7) dft7<INV>(v);
   else if constexpr (R == 8) dft8<INV>(v);
   else if constexpr (R == 16) dft16<INV>(v);
-  else if constexpr (R == 15) dft_ct<3, 5, INV>(v);
-  else if constexpr (R == 20) dft_ct<4, 5, INV>(v);
-  else if constexpr (R == 12) dft_ct<4, 3, INV>(v);
   else static_assert(R == 0, "no in-register DFT of this radix");
 }
 
@@ -592,18 +471,11 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
 // from either lane-pair form: the tail spills at 64 VGPRs (K3 2.19 -> 2.62 ms); the head (MODE 3,
 // one LDS exchange fewer, no input twiddles) leaves a full radix-16 last stage whose twiddles and
 // cropped stores spill at 64 VGPRs (3.31 ms) and run 2.32 ms at 7 waves/SIMD without spills --
-// so the row passes are not LDS-exchange-bound and keep MODE 0 (THZ_ROWS_MODE).  fft_rows_kernel
+// so the row passes are not LDS-exchange-bound and keep MODE 0 (FFT_ROWS).  fft_rows_kernel
 // (diagnostics) runs MODE 2 forward and MODE 3 inverse so both split-image forms stay tested.
-#ifndef THZ_PAIR32
-#define THZ_PAIR32 1
-#endif
-// Row passes (split image): THZ_ROWS_MODE 3 puts the lane-pair radix 32 first (decimation in
-// frequency), 2 last, 0 neither (the default, measured above).
-#ifndef THZ_ROWS_MODE
-#define THZ_ROWS_MODE 0
-#endif
-constexpr int FFT_TAIL = THZ_PAIR32 ? 2 : 0;
-constexpr int FFT_ROWS = THZ_ROWS_MODE;
+// The column pass's inverse uses MODE 2; the row passes MODE 0 (measured above).
+constexpr int FFT_TAIL = 2;
+constexpr int FFT_ROWS = 0;
 template <int N>
 struct Pow2Sched {
   static constexpr int log2n() {
@@ -942,19 +814,15 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
   }
 }
 
-// The row / column kernels' transform: split exchanges (THZ_SPLIT, the default) or the complex
-// image; tw_slot is where that kernel's twiddle tables start in LDS.
+// The row / column kernels' transform runs the split exchanges; tw_slot is where that kernel's
+// twiddle tables start in LDS.
 template <int N>
 __device__ __forceinline__ float2* tw_slot(float2* lds) {
-  return lds + (THZ_SPLIT ? lds_split_f2(N) : lds_floats2(N));
+  return lds + lds_split_f2(N);
 }
 template <bool INV, int N, int T, int MODE, class Tw, class Ld, class Sv>
 __device__ __forceinline__ void fft_pow2_run(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
-#if THZ_SPLIT
   fft_pow2_split_io<INV, N, T, MODE>(reinterpret_cast<float*>(lds), tw, tid, ld, sv);
-#else
-  fft_pow2_io<INV, N, T, MODE, false, false>(lds, tw, tid, ld, sv);
-#endif
 }
 
 // Whole transform with the data in LDS (natural order in and out).
@@ -974,9 +842,6 @@ __device__ __forceinline__ void fft_pow2(float2* lds, const Tw& tw, int tid) {
 // therefore reads exactly the elements the previous transform left in this thread's registers.
 // Twiddles exp(-+2 pi i k t / N) come from the plan's global table (L2-resident, N float2).
 // ---------------------------------------------------------------------------------------------
-#ifndef THZ_MX_TWR
-#define THZ_MX_TWR 1  // stage twiddles held in registers (1) or read from the table per stage (0)
-#endif
 template <bool INV, int N, int T, int L, int R, bool FIRST, bool LAST, int MW, class Ld, class Sv>
 __device__ __forceinline__ void mx_stage(float2* lds, const float2 (&w1)[MW], const float2* __restrict__ tw, int tid,
                                          Ld& ld, Sv& sv) {
@@ -994,7 +859,7 @@ __device__ __forceinline__ void mx_stage(float2* lds, const float2 (&w1)[MW], co
         else v[m][r] = lds[padx(i + r * NB)];
       }
       if constexpr (L > 1) {
-        const float2 w = THZ_MX_TWR ? w1[m] : tw[(i % L) * (N / (L * R))];
+        const float2 w = w1[m];
         float2 wr = w;
 #pragma unroll
         for (int r = 1; r < R; ++r) {
@@ -1049,7 +914,6 @@ struct MxTw {
   const float2* tw;
   template <int L, int S, int R, int... Rest>
   __device__ __forceinline__ void fill(const float2* __restrict__ tw, int tid) {
-    if (!THZ_MX_TWR) return;
     constexpr int NB = N / R, MB = (NB + T - 1) / T;
 #pragma unroll
     for (int m = 0; m < MW; ++m) {
@@ -1082,11 +946,8 @@ struct MxPlan {
 };
 // 300 = 5 3 4 5: first and last radix 5 (60 butterflies: one per lane of a 64-thread workgroup),
 // so the forward's spectrum is 5 values per lane and the inverse starts from it directly
-#ifndef THZ_MX_PLAN
-#define THZ_MX_PLAN 0
-#endif
-using Mx300 = std::conditional_t<THZ_MX_PLAN == 0, MxPlan<5, 3, 4, 5>,
-                                 std::conditional_t<THZ_MX_PLAN == 1, MxPlan<5, 4, 3, 5>, MxPlan<5, 12, 5>>>;
+// (5 4 3 5 and 5 12 5 measured within noise / slower)
+using Mx300 = MxPlan<5, 3, 4, 5>;
 
 // Full transform of one row held in LDS (natural order in and out).  Unnormalised.
 template <bool INV>
