@@ -328,7 +328,12 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       asm volatile("" : "+v"(tz));
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
+      // the first stage's operands r in [4, 12) are the rows PN/4 <= |m_x| < 3 PN/4: when this
+      // plane's kept band M is below PN/4 (all but the few columns near m_y = 0 at cfg2) they are
+      // zero for every thread, and a scalar branch skips their sincos and product
+      const bool mid0 = __builtin_amdgcn_readfirstlane(M) < PN / 4;
       auto ld1 = [&](int m, int r, int idx) {
+        if (RL == 16 && r >= 4 && r < 12 && mid0) return make_float2(0.f, 0.f);
         const int mx = freq_index(idx, PN);
         if (mx > M || -mx > M) return make_float2(0.f, 0.f);
         float sn, cs;
@@ -541,7 +546,13 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
     static_assert(Geo<PN>::T == NB0, "one first-stage butterfly per thread: i = tid");
     const int c0 = tid + a.J;
     const float2* base = src + ((long)(c0 / CBU) * a.Hout + r) * CBU + (c0 % CBU);
+    // operands q in [4, 12) are the columns PN/4 <= |m_y| < 3 PN/4: outside the band for every
+    // lane of most waves (all but the first and last at cfg2), which then skip their address math
+    // and masked loads on one scalar branch
+    static_assert(NB0 == PN / 16, "radix-16 first stage");
+    const bool mid0 = __all(c0 + 4 * NB0 >= a.ncols && c0 + 11 * NB0 - PN < 0);
     auto ld = [&](int, int q, int) {
+      if (q >= 4 && q < 12 && mid0) return make_float2(0.f, 0.f);
       const int delta = q * NB0 >= PN / 2 ? q * NB0 - PN : q * NB0;
       if ((unsigned)(c0 + delta) >= (unsigned)a.ncols) return make_float2(0.f, 0.f);
       return base[(long)delta * a.Hout];
