@@ -10,13 +10,14 @@ import sys
 
 __version__ = "0.1.0"
 
-_ALIASES = ("DataType", "Props", "Components", "LightSource", "utils", "Addons")
+_ALIASES = ("DataType", "Props", "Components", "LightSource", "utils", "Addons", "VisTools")
 
 
 _MODULES = ("DataType.ElectricField", "Props.ASM_Prop", "Props.CZT_Prop", "Props.RSC_Prop",
             "Components.QuantizedDOE", "Components.Thin_Lens", "Components.Aperture",
             "LightSource.Gaussian_beam", "Addons.Field_Resampler", "Addons.Field_Crop",
-            "utils.units", "utils.Visualization_Helper", "utils.Helper_Functions")
+            "utils.units", "utils.Visualization_Helper", "utils.Helper_Functions",
+            "VisTools.directions", "VisTools.calc_loss")
 
 
 def install_reference_aliases():
