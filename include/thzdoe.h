@@ -158,6 +158,19 @@ int thz_doe_modulate_backward(const thz_doe_desc* d, const void* grad_out, const
                               const float* noise, void* grad_field, float* grad_height, thz_stream_t stream);
 
 /*
+ * Fused DOE -> ASM step: the ASM forward of thz_doe_modulate_forward(field) in one
+ * pipeline -- the row pass applies the noisy, upsampled transmission t_c(h) in its loader, so the
+ * modulated field never goes to memory.  Replaces DOELayer.modulate (Components/QuantizedDOE.py:
+ * 92-126) followed by ASM_prop.forward (Props/ASM_Prop.py:314-378).  d: the ASM descriptor (forward,
+ * adjoint == 0); m: the DOE descriptor of the same [B, C, H, W] field.  height_full (optional)
+ * receives the noisy upsampled height map [H, W].  The backward composes the ASM adjoint and
+ * thz_doe_modulate_backward.
+ */
+int thz_asm_forward_modulated(const thz_asm_desc* d, const thz_doe_desc* m, const void* field, const float* height,
+                              const float* noise, float* height_full, void* out, void* workspace,
+                              size_t workspace_bytes, thz_stream_t stream);
+
+/*
  * Height-map quantizers of the QAT layers (forward value + custom backward), one fused kernel
  * each way.  weight: [hq, wq] (FP/STE/PSQ/SGV3) or [hq, wq, L] logits (NGS).  height_full:
  * [2hq, 2wq] when mirror (num_unit set, _copy_quad_to_full :28-35) else [hq, wq].

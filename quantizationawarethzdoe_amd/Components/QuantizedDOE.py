@@ -94,16 +94,32 @@ class DOELayer(nn.Module):
         return 0
 
     def modulate(self, input_field, preprocessed_height_map, height_tolerance, epsilon, tand) -> ElectricField:
-        """Noise + nearest upsampling + transmission + product in one kernel (:92-126)."""
+        """Noise + nearest upsampling + transmission + product (:92-126).  The noise is drawn here (the
+        reference's RNG order); the product is left pending on the returned field: a following
+        ASM_prop forms it inside its row pass (one pipeline), any other reader of
+        ``.data`` forms it with the modulate kernel."""
         h = preprocessed_height_map
         if h.dim() != 2:
             h = h.reshape(h.shape[-2:])
         tol = None if height_tolerance is None else self._host_scalar("tol", height_tolerance)
-        out, self._height_map_ = _doe.modulate(input_field.data, h, input_field.wavelengths_host,
-                                               self._host_scalar("eps", epsilon), self._host_scalar("tand", tand),
-                                               tolerance=tol)
-        return ElectricField(data=out, wavelengths=input_field.wavelengths,
-                             spacing=input_field.spacing)._adopt_host(input_field)
+        data = input_field.data
+        self._pending_mod = _doe.PendingModulation(data, h, input_field.wavelengths_host,
+                                                   self._host_scalar("eps", epsilon), self._host_scalar("tand", tand),
+                                                   tolerance=tol)
+        out = ElectricField(data=data, wavelengths=input_field.wavelengths,
+                            spacing=input_field.spacing)._adopt_host(input_field)
+        out._pending = self._pending_mod
+        return out
+
+    @property
+    def _height_map_(self):
+        """The noisy, upsampled height map of the last forward (DOELayer.modulate :102-107)."""
+        pend = self.__dict__.get("_pending_mod")
+        if pend is None:
+            return None
+        if pend.hfull is None:
+            pend.run()
+        return pend.hfull
 
     # -- shared helpers ------------------------------------------------------------------------
     def _host_scalar(self, key, v):

@@ -28,6 +28,9 @@ class ElectricField:
     _WAVELENGTH = 1
     _HEIGHT = 2
     _WIDTH = 3
+    # MI355X addition: a DOE layer's output may carry its modulation unevaluated (doe.PendingModulation);
+    # the next ASM_prop then applies it inside its row pass, anything else that reads .data forms it
+    _pending = None
 
     def __init__(self, data: torch.Tensor, wavelengths: Union[torch.Tensor, float] = None,
                  spacing: Union[torch.Tensor, float] = None, requires_grad: bool = None, device=None):
@@ -58,15 +61,23 @@ class ElectricField:
 
     @property
     def requires_grad(self):
-        return self._data.requires_grad
+        return self.data.requires_grad
 
     @property
     def data(self) -> torch.Tensor:
+        if self._pending is not None:
+            pend, self._pending = self._pending, None
+            self._data = pend.run()
         return self._data
 
     @data.setter
     def data(self, data):
+        self._pending = None
         self._data = self.check_data(data)
+
+    def _take_pending(self):
+        """The unevaluated modulation this field carries (None once its data has been formed)."""
+        return self._pending
 
     # -- host mirrors of the physical scalars (MI355X addition) --------------------------------
     @property
@@ -142,16 +153,16 @@ class ElectricField:
         return f._adopt_host(self)
 
     def abs(self) -> "ElectricField":
-        return self._like(self._data.abs())
+        return self._like(self.data.abs())
 
     def angle(self) -> "ElectricField":
-        return self._like(self._data.angle())
+        return self._like(self.data.angle())
 
     def detach(self) -> "ElectricField":
-        return self._like(self._data.detach(), self._wavelengths.detach(), self._spacing.detach())
+        return self._like(self.data.detach(), self._wavelengths.detach(), self._spacing.detach())
 
     def cpu(self) -> "ElectricField":
-        return ElectricField(data=self._data.cpu(), wavelengths=self._wavelengths.detach(),
+        return ElectricField(data=self.data.cpu(), wavelengths=self._wavelengths.detach(),
                              spacing=self._spacing.detach(), device=self.device)
 
     # -- shape accessors (DataType/ElectricField.py:169-203) ----------------------------------
@@ -181,19 +192,19 @@ class ElectricField:
 
     @property
     def Ex(self):
-        return self._data[[0], ...]
+        return self.data[[0], ...]
 
     @property
     def Ey(self):
-        return self._data[[1], ...]
+        return self.data[[1], ...]
 
     @property
     def Ez(self):
-        return self._data[[2], ...]
+        return self.data[[2], ...]
 
     def _get_data_for_wavelength(self, wavelength):
         idx = (self._wavelengths == wavelength).nonzero()[0]
-        return self._data[:, idx, ...]
+        return self.data[:, idx, ...]
 
     def visualize(self, flag_colorbar: bool = True, flag_axis: str = True, cmap="viridis", wavelength=None,
                   figsize=(8, 8), intensity=True):

@@ -124,7 +124,8 @@ class ASM_prop(nn.Module):
         self.check_Zc = False
 
     def _run(self, field: ElectricField, zs):
-        data = field.data
+        pend = field._take_pending()
+        data = pend.field if pend is not None else field.data
         B, C, H, W = data.shape
         ph, pw = self.compute_padding(H, W, return_size_of_padding=True)
         bl = self._bandlimit_code()
@@ -132,9 +133,13 @@ class ASM_prop(nn.Module):
         sp = field.spacing_host
         self._zc_diagnostic(H + 2 * ph, sp[0], wl, zs[0])
         x = _prop.kernel_dtype(data, "ASM_prop", field.wavelengths)
+        unpad = (not self.do_padding) or self.do_unpad_after_pad
         try:
-            out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=(not self.do_padding) or self.do_unpad_after_pad,
-                                      bandlimit=bl)
+            if pend is not None and pend.out is None:  # the DOE layer's modulation, fused into the row pass
+                out = _prop.asm_propagate_modulated(pend, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl)
+            else:
+                x = pend.run() if pend is not None else x
+                out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl)
         except RuntimeError as err:
             print("##################################################")
             print("An error occurred.  If the error was due to insufficient memory, try decreasing the size of the "

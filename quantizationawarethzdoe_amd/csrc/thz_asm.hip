@@ -50,6 +50,12 @@ struct AsmArgs {
   float zr;           // VRS: z of the Ez grid
   float* sqt;         // mixed-radix K2: sqrt(k^2 - Kx^2 - Ky^2) per [C][ncols][Ph] (asm_tf_tables)
   int* mzt;           // mixed-radix K2: kept-row bound M_z per [C][ncols][nz] of the current z-chunk
+  // fused DOE modulation in the row pass (thz_asm_forward_modulated): the input row is field * t_c(h)
+  const float* mod_h;   // height map [mod_hs][mod_ws] (nullptr: no modulation)
+  const float* mod_u;   // U[0,1) height-noise draw, same shape (nullptr: no noise)
+  float* mod_hfull;     // optional: the noisy, upsampled height map [Hin][Win]
+  int mod_hs, mod_ws;
+  float mod_tol, mod_eps, mod_tand;
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
@@ -175,7 +181,14 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
   const float2* sx = in + ((size_t)(bc % a.C) * a.Hin + h) * a.Win;
   const float2* sy = in + ((size_t)(a.C + bc % a.C) * a.Hin + h) * a.Win;
   const float xh = ez ? lin(-(float)a.Hin * a.dx / 2.0f, (float)a.Hin * a.dx / 2.0f, a.Hin, h) : 0.f;
+  const int hsrc = a.mod_h ? doe_nearest_src(h, a.mod_hs, a.Hin) * a.mod_ws : 0;
+  const float lam_c = a.lam[bc % a.C];
   auto fetch = [&](int s) {
+    if (a.mod_h) {  // DOELayer.modulate fused into the loader (Components/QuantizedDOE.py:92-126)
+      const float hv = doe_noisy_h(a.mod_h, a.mod_u, hsrc + doe_nearest_src(s, a.mod_ws, a.Win), a.mod_tol);
+      if (a.mod_hfull && bc == 0) a.mod_hfull[(size_t)h * a.Win + s] = hv;
+      return cmul(src[s], doe_transmission(hv, lam_c, a.mod_eps, a.mod_tand, nullptr));
+    }
     if (!ez) return src[s];
     return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
   };
@@ -938,8 +951,10 @@ extern "C" int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes) {
   return THZ_OK;
 }
 
-extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* workspace,
-                               size_t workspace_bytes, thz_stream_t stream) {
+namespace thz {
+static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const float* mh, const float* mu,
+                            float* mhfull, const void* in, void* out, void* workspace, size_t workspace_bytes,
+                            thz_stream_t stream) {
   int e = validate(d);
   if (e) return e;
   if (!in || !out) return fail(THZ_E_ARG, "null data pointer");
@@ -977,11 +992,39 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
   a.scale = (float)(1.0 / ((double)g.Ph * (double)g.Pw));
   for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
   for (int zi = 0; zi < d->Z; ++zi) a.zv[zi] = d->z[zi];
+  if (m) {
+    a.mod_h = mh;
+    a.mod_u = mu;
+    a.mod_hfull = mhfull;
+    a.mod_hs = m->hs;
+    a.mod_ws = m->ws;
+    a.mod_tol = m->tolerance;
+    a.mod_eps = m->epsilon;
+    a.mod_tand = m->tand;
+  }
 
   float2* T = (float2*)workspace;
   float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
   char* tabs = (char*)workspace + ws_bytes(g) - tab_bytes(g);
   return run_pipeline(a, g, d->Z, in, out, T, U, (hipStream_t)stream, pw, ph, tab_bytes(g) ? tabs : nullptr);
+}
+}  // namespace thz
+
+extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* workspace,
+                               size_t workspace_bytes, thz_stream_t stream) {
+  return asm_forward_impl(d, nullptr, nullptr, nullptr, nullptr, in, out, workspace, workspace_bytes, stream);
+}
+
+extern "C" int thz_asm_forward_modulated(const thz_asm_desc* d, const thz_doe_desc* m, const void* field,
+                                         const float* height, const float* noise, float* height_full, void* out,
+                                         void* workspace, size_t workspace_bytes, thz_stream_t stream) {
+  if (!d || !m || !height) return fail(THZ_E_ARG, "null descriptor / height");
+  if (d->adjoint) return fail(THZ_E_ARG, "the fused DOE modulation is forward only");
+  if (m->B != d->B || m->C != d->C || m->H != d->H || m->W != d->W)
+    return fail(THZ_E_ARG, "DOE field %dx%dx%dx%d does not match the ASM input %dx%dx%dx%d", m->B, m->C, m->H, m->W,
+                d->B, d->C, d->H, d->W);
+  if (m->hs < 1 || m->ws < 1) return fail(THZ_E_ARG, "bad height-map size %dx%d", m->hs, m->ws);
+  return asm_forward_impl(d, m, height, noise, height_full, field, out, workspace, workspace_bytes, stream);
 }
 
 namespace thz {

@@ -160,4 +160,42 @@ __device__ __forceinline__ float lin(float start, float end, int n, int i) {
 
 
 
+// ---------------------------------------------------------------------------------------------
+// DOE transmission (Components/QuantizedDOE.py:47-126), shared by the modulate kernels
+// (thz_doe.hip) and the ASM row pass that applies it in its loader (thz_asm.hip, the fused
+// DOE -> ASM step).  fp32 in the reference's operation order.
+// ---------------------------------------------------------------------------------------------
+constexpr float DOE_BASE_PLANE = 2e-3f;  // BASE_PLANE_THICKNESS (:23)
+
+#pragma clang fp contract(off)
+// nearest source index of torch.nn.functional.interpolate(mode='nearest'), fp32 scale (:102-107)
+__device__ __forceinline__ int doe_nearest_src(int dst, int in, int out) {
+  if (in == out) return dst;
+  const float scale = (float)in / (float)out;
+  return min((int)floorf((float)dst * scale), in - 1);
+}
+
+// noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85); u == nullptr: no noise
+__device__ __forceinline__ float doe_noisy_h(const float* h, const float* u, int idx, float tol) {
+  float v = h[idx];
+  if (u) v = v + ((u[idx] - 0.5f) * 2.0f) * tol;
+  return v;
+}
+
+// t_c(h) and gamma_c = dt/dh / t (:73-77)
+__device__ __forceinline__ float2 doe_transmission(float hv, float lam, float eps, float tand, float2* gamma) {
+  const float k = 6.283185307179586f / lam;
+  const float hb = hv + DOE_BASE_PLANE;
+  const float se = sqrtf(eps);
+  const float ga = ((-0.5f * k) * tand) * se;  // d(log loss)/dh
+  const float loss = expf(((-0.5f * k) * hb * tand) * se);
+  const float gb = -k * (se - 1.0f);           // d(phase)/dh
+  const float ph = (-k * hb) * (se - 1.0f);
+  float sn, cs;
+  sincos_rad(ph, &sn, &cs);
+  if (gamma) *gamma = make_float2(ga, gb);
+  return make_float2(loss * cs, loss * sn);
+}
+#pragma clang fp contract(on)
+
 }  // namespace thz

@@ -28,7 +28,6 @@
 
 namespace thz {
 
-constexpr float BASE_PLANE = 2e-3f;  // BASE_PLANE_THICKNESS (:23)
 
 struct ModArgs {
   int B, C, H, W, hs, ws;
@@ -38,34 +37,12 @@ struct ModArgs {
   float lam[THZ_MAX_WAVELENGTHS];
 };
 
-#pragma clang fp contract(off)
-// nearest source index of torch.nn.functional.interpolate(mode='nearest'), fp32 scale
-__device__ __forceinline__ int nearest_src(int dst, int in, int out) {
-  if (in == out) return dst;
-  const float scale = (float)in / (float)out;
-  return min((int)floorf((float)dst * scale), in - 1);
-}
-
-// noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85)
+__device__ __forceinline__ int nearest_src(int dst, int in, int out) { return doe_nearest_src(dst, in, out); }
 __device__ __forceinline__ float noisy_h(const float* h, const float* u, int idx, const ModArgs& a) {
-  float v = h[idx];
-  if (a.has_noise) v = v + ((u[idx] - 0.5f) * 2.0f) * a.tol;
-  return v;
+  return doe_noisy_h(h, a.has_noise ? u : nullptr, idx, a.tol);
 }
-
-// t_c(h) and gamma_c = dt/dh / t (:73-77)
 __device__ __forceinline__ float2 transmission(float hv, float lam, const ModArgs& a, float2* gamma) {
-  const float k = 6.283185307179586f / lam;
-  const float hb = hv + BASE_PLANE;
-  const float se = sqrtf(a.eps);
-  const float ga = ((-0.5f * k) * a.tand) * se;  // d(log loss)/dh
-  const float loss = expf(((-0.5f * k) * hb * a.tand) * se);
-  const float gb = -k * (se - 1.0f);             // d(phase)/dh
-  const float ph = (-k * hb) * (se - 1.0f);
-  float sn, cs;
-  sincos_rad(ph, &sn, &cs);
-  if (gamma) *gamma = make_float2(ga, gb);
-  return make_float2(loss * cs, loss * sn);
+  return doe_transmission(hv, lam, a.eps, a.tand, gamma);
 }
 
 // grid (pixel blocks, batch stride): t_c(h) once per pixel, thread and wavelength

@@ -53,28 +53,68 @@ class _Modulate(torch.autograd.Function):
     def backward(ctx, g, _gh):
         field, height, noise = ctx.saved_tensors
         tol, eps, tand, wavelengths = ctx.cfg
-        B, C, H, W = field.shape
-        hs, ws = height.shape
-        d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths)
-        g = g.contiguous()
-        gf = torch.empty_like(field) if ctx.needs_input_grad[0] else None
-        gh = torch.empty((hs, ws), dtype=torch.float32, device=field.device) if ctx.needs_input_grad[1] else None
-        with torch.cuda.device(field.device):
-            _lib.check(_lib.lib().thz_doe_modulate_backward(ctypes.byref(d), _ptr(g), _ptr(field), _ptr(height),
-                                                            _ptr(noise), _ptr(gf), _ptr(gh), _stream_handle()))
-        return gf, gh, None, None, None, None, None
+        return modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, ctx.needs_input_grad[0],
+                                 ctx.needs_input_grad[1]) + (None, None, None, None, None)
 
 
-def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None):
-    """Differentiable DOE modulation on the HIP kernel; returns (out, noisy full-size height)."""
+def modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, need_field=True, need_height=True):
+    """(grad_field, grad_height) of field * t(h + noise) for the output gradient g (one kernel)."""
+    B, C, H, W = field.shape
+    hs, ws = height.shape
+    d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths)
+    g = g.contiguous()
+    gf = torch.empty_like(field) if need_field else None
+    gh = torch.empty((hs, ws), dtype=torch.float32, device=field.device) if need_height else None
+    with torch.cuda.device(field.device):
+        _lib.check(_lib.lib().thz_doe_modulate_backward(ctypes.byref(d), _ptr(g), _ptr(field), _ptr(height),
+                                                        _ptr(noise), _ptr(gf), _ptr(gh), _stream_handle()))
+    return gf, gh
+
+
+def _modulate_args(field, height, tolerance, noise):
     from quantizationawarethzdoe_amd.propagation import kernel_dtype
     field = kernel_dtype(field, "DOE modulate")
     if tolerance is not None and noise is None:
         noise = torch.rand_like(height)
     if noise is not None:
         noise = noise.detach().contiguous().float()
-    tol = 0.0 if tolerance is None else float(tolerance)
+    return field, noise, 0.0 if tolerance is None else float(tolerance)
+
+
+def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None):
+    """Differentiable DOE modulation on the HIP kernel; returns (out, noisy full-size height)."""
+    field, noise, tol = _modulate_args(field, height, tolerance, noise)
     return _Modulate.apply(field, height, noise, tol, float(eps), float(tand), tuple(map(float, wavelengths)))
+
+
+class PendingModulation:
+    """A DOELayer.modulate whose product has not been formed yet.  The noise is drawn
+    when the layer runs (the reference's RNG order); the product is formed either by the next
+    ASM_prop, inside its row pass (thz_asm_forward_modulated: the modulated field never goes to
+    memory), or by ``run()`` -- the plain modulate kernel -- the first time anything reads the
+    field's data.  ``hfull`` is the noisy upsampled height map, set by whichever runs first."""
+
+    def __init__(self, field, height, wavelengths, eps, tand, tolerance=None, noise=None):
+        self.field, self.noise, self.tol = _modulate_args(field, height, tolerance, noise)
+        self.height = height
+        self.wavelengths = tuple(map(float, wavelengths))
+        self.eps, self.tand = float(eps), float(tand)
+        self.out = None
+        self.hfull = None
+
+    def run(self):
+        if self.out is None:
+            self.out, hf = _Modulate.apply(self.field, self.height, self.noise, self.tol, self.eps, self.tand,
+                                           self.wavelengths)
+            if self.hfull is None:
+                self.hfull = hf
+        return self.out
+
+    def desc(self):
+        """The thz_doe_desc of this modulation (+ the arrays it points to kept alive)."""
+        B, C, H, W = self.field.shape
+        hs, ws = self.height.shape[-2:]
+        return _doe_desc(B, C, H, W, hs, ws, self.tol, self.eps, self.tand, self.wavelengths)
 
 
 def _quant_desc(kind, hq, wq, mirror, lut, hmax, clamp, tau=1.0, iter_frac=0.0, c_s=0.0, s=0.0, beta=0.0,

@@ -134,6 +134,64 @@ def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, band
                               list(map(float, zs)), int(pad_h), int(pad_w), bool(unpad), bl, int(z_chunk))
 
 
+class _AsmModulatedFunction(torch.autograd.Function):
+    """ASM forward of DOELayer.modulate(field) in one pipeline (thz_asm_forward_modulated): the row
+    pass applies t_c(h + noise) in its loader.  Backward: the ASM adjoint per plane, then the
+    modulate backward kernel (grad_field, grad_height)."""
+
+    @staticmethod
+    def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
+        _require_device(field, "ASM")
+        field = field.contiguous()
+        h = height.detach().contiguous().float()
+        B, C, H, W = field.shape
+        Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
+        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False)
+        m = pend.desc()
+        L = _lib.lib()
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+        ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=field.device)
+        out = torch.empty((len(zs), B, C, Ho, Wo), dtype=torch.complex64, device=field.device)
+        hfull = torch.empty((H, W), dtype=torch.float32, device=field.device)
+        noise = pend.noise
+        with torch.cuda.device(field.device):
+            _lib.check(L.thz_asm_forward_modulated(
+                ctypes.byref(d), ctypes.byref(m), ctypes.c_void_p(field.data_ptr()), ctypes.c_void_p(h.data_ptr()),
+                ctypes.c_void_p(noise.data_ptr() if noise is not None else 0), ctypes.c_void_p(hfull.data_ptr()),
+                ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()),
+                _stream_handle()))
+        if pend.hfull is None:
+            pend.hfull = hfull
+        ctx.save_for_backward(field, h)
+        ctx.pend = pend
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from . import doe as _doe
+        field, h = ctx.saved_tensors
+        pend = ctx.pend
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
+        g = g.contiguous()
+        gm = None
+        for k, z in enumerate(zs):
+            gk = asm_apply(g[k:k + 1], wavelengths, spacing, [z], pad_h, pad_w, unpad, bandlimit, True)
+            gm = gk if gm is None else gm + gk
+        gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
+                                        ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return gf, gh, None, None, None, None, None, None, None, None
+
+
+def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact"):
+    """Differentiable fused DOE modulation + ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo]."""
+    bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
+    return _AsmModulatedFunction.apply(pend.field, pend.height, pend, list(map(float, wavelengths)),
+                                       tuple(map(float, spacing)), list(map(float, zs)), int(pad_h), int(pad_w),
+                                       bool(unpad), bl)
+
+
 def fft_rows(x, inverse=False):
     """Unnormalised batched 1-D FFT along the last axis with the LDS Stockham kernel."""
     _require_device(x, "fft_rows")

@@ -262,3 +262,41 @@ def test_complex128_rejected():
     x = torch.ones(1, 1, 8, 8, dtype=torch.complex128, device=_dev())
     with pytest.raises(TypeError):
         doe.modulate(x, torch.zeros(8, 8, device=_dev()), [1e-3], 2.66, 0.03)
+
+
+@pytest.mark.parametrize("shape,dsize", [((2, 2, 60, 60), (30, 30)), ((1, 1, 100, 100), (100, 100))])
+def test_fused_modulate_asm_equals_separate(shape, dsize):
+    """DOE layer -> ASM_prop runs fused (the modulation applied in the ASM row pass, SURVEY §8(f)1);
+    forcing the modulated field first (reading .data) runs the separate modulate kernel.  Same noise
+    draws (seeded), same outputs, same gradients for the weight and the input field."""
+    from quantizationawarethzdoe_amd.Components.QuantizedDOE import FullPrecisionDOELayer
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    dev = _dev()
+    B, C, H, W = shape
+    dp = {'doe_size': list(dsize), 'doe_dxy': 1e-3, 'doe_level': 4, 'look_up_table': None, 'num_unit': None,
+          'height_constraint_max': 1e-3, 'tolerance': 1e-5, 'material': [2.66, 0.03]}
+    torch.manual_seed(0)
+    layer = FullPrecisionDOELayer(dp, device=dev)
+    asm = ASM_prop(z_distance=0.15, padding_scale=2, device=dev)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(shape, dtype=torch.complex64, generator=g).to(dev)
+    gout = torch.randn(shape, dtype=torch.complex64, generator=g).to(dev)
+    wl = [2.998e8 / 300e9, 2.998e8 / 250e9][:C]
+    res = []
+    for fused in (True, False):
+        xd = x.clone().requires_grad_(True)
+        layer.weight_height_map.grad = None
+        torch.manual_seed(7)
+        f = layer(ElectricField(xd, wavelengths=wl if C > 1 else wl[0], spacing=1e-3, device=dev), 0.5)
+        assert f._pending is not None
+        if not fused:
+            _ = f.data  # form the modulated field with the modulate kernel
+        out = asm(f).data
+        out.backward(gout)
+        res.append((out.detach().cpu(), xd.grad.cpu(), layer.weight_height_map.grad.cpu(), layer._height_map_.cpu()))
+    (o1, gx1, gw1, h1), (o2, gx2, gw2, h2) = res
+    assert torch.equal(h1, h2)
+    assert rel_l2(o1.numpy(), o2.numpy()) <= 1e-6
+    assert rel_l2(gx1.numpy(), gx2.numpy()) <= 1e-6
+    assert rel_l2(gw1.numpy(), gw2.numpy()) <= 1e-5
