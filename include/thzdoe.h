@@ -272,6 +272,21 @@ int thz_intensity_mse_backward(const thz_loss_desc* d, const void* field, const 
                                const float* grad_loss, void* grad_field, thz_stream_t stream);
 
 /*
+ * Fused ASM -> loss step: ASM forward of one z-plane (optionally of the DOE
+ * modulation of field, as thz_asm_forward_modulated; m == NULL: plain ASM, height / noise /
+ * height_full ignored) whose row-inverse pass also accumulates the QAT loss above over the rows
+ * it stores, so the output field is not read back.  Replaces ASM_prop.forward (Props/
+ * ASM_Prop.py:314-378) followed by the notebook's loss (experiment_four_focal_spots.ipynb:
+ * 336-370, normalize = utils/Helper_Functions.py:185-193).  l describes the ASM output
+ * [B, C, Ho, Wo]; out, loss and stats are what thz_asm_forward and thz_intensity_mse_forward
+ * return (stats: thz_intensity_mse_workspace_size bytes, valid for thz_intensity_mse_backward).
+ */
+int thz_asm_forward_loss(const thz_asm_desc* d, const thz_doe_desc* m, const void* field, const float* height,
+                         const float* noise, float* height_full, const thz_loss_desc* l, const float* target,
+                         void* out, float* loss, float* stats, void* workspace, size_t workspace_bytes,
+                         thz_stream_t stream);
+
+/*
  * Field_Resampler.forward (Addons/Field_Resampler.py:74-118): bilinear grid_sample (zeros
  * padding, align_corners=True) of [BC, Hin, Win] complex64 onto the centred output grid
  * linspace(-((n-1)//2), (n-1)//2, n) * d_out, normalised by d_in * ((n_in - 1) // 2).

@@ -29,7 +29,9 @@ class ElectricField:
     _HEIGHT = 2
     _WIDTH = 3
     # MI355X addition: a DOE layer's output may carry its modulation unevaluated (doe.PendingModulation);
-    # the next ASM_prop then applies it inside its row pass, anything else that reads .data forms it
+    # the next ASM_prop then applies it inside its row pass, anything else that reads .data forms it.
+    # Inside propagation.deferred_output() an ASM_prop output carries its propagation unevaluated
+    # (Props.ASM_Prop._PendingAsm) so the QAT loss can be folded into it (optics.field_intensity_mse).
     _pending = None
 
     def __init__(self, data: torch.Tensor, wavelengths: Union[torch.Tensor, float] = None,
@@ -77,7 +79,17 @@ class ElectricField:
 
     def _take_pending(self):
         """The unevaluated modulation this field carries (None once its data has been formed)."""
-        return self._pending
+        p = self._pending
+        return p if getattr(p, "kind", None) == "modulation" else None
+
+    def _take_pending_propagation(self):
+        """The deferred ASM_prop.forward this field is the output of (propagation.deferred_output),
+        detached from the field: the caller forms the data (and sets it) itself."""
+        p = self._pending
+        if getattr(p, "kind", None) != "propagation":
+            return None
+        self._pending = None
+        return p
 
     # -- host mirrors of the physical scalars (MI355X addition) --------------------------------
     @property

@@ -33,6 +33,22 @@ def _z_host(z):
     return [float(z)]
 
 
+class _PendingAsm:
+    """An ASM_prop.forward not yet run (propagation.deferred_output): ``run()`` gives the field
+    data as forward would; ``run_loss(target)`` gives (data, QAT loss) from the fused pipeline."""
+    kind = "propagation"
+
+    def __init__(self, prop, field, zs):
+        self.prop, self.field, self.zs = prop, field, zs
+
+    def run(self):
+        return self.prop._run(self.field, self.zs)[0]
+
+    def run_loss(self, target):
+        out, loss = self.prop._run(self.field, self.zs, loss_target=target)
+        return out[0], loss
+
+
 class ASM_prop(nn.Module):
     def __init__(self, z_distance: float = 0.0, do_padding: bool = True, do_unpad_after_pad: bool = True,
                  padding_scale=None, bandlimit_kernel: bool = True, bandlimit_type: str = "exact",
@@ -123,7 +139,8 @@ class ASM_prop(nn.Module):
             print("The critical distance is {} m, the TF will be fine during the sampling !".format(zc))
         self.check_Zc = False
 
-    def _run(self, field: ElectricField, zs):
+    def _run(self, field: ElectricField, zs, loss_target=None):
+        """[Z, B, C, Ho, Wo]; with ``loss_target`` (one z): (out, QAT loss) from the fused pipeline."""
         pend = field._take_pending()
         data = pend.field if pend is not None else field.data
         B, C, H, W = data.shape
@@ -135,7 +152,12 @@ class ASM_prop(nn.Module):
         x = _prop.kernel_dtype(data, "ASM_prop", field.wavelengths)
         unpad = (not self.do_padding) or self.do_unpad_after_pad
         try:
-            if pend is not None and pend.out is None:  # the DOE layer's modulation, fused into the row pass
+            if loss_target is not None:
+                fuse = pend is not None and pend.out is None
+                x = pend.run() if pend is not None and not fuse else x
+                out = _prop.asm_propagate_loss(x, loss_target, wl, sp, zs[0], ph, pw, unpad=unpad, bandlimit=bl,
+                                               pend=pend if fuse else None)
+            elif pend is not None and pend.out is None:  # the DOE layer's modulation, fused into the row pass
                 out = _prop.asm_propagate_modulated(pend, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl)
             else:
                 x = pend.run() if pend is not None else x
@@ -151,7 +173,21 @@ class ASM_prop(nn.Module):
         return out
 
     def forward(self, field: ElectricField) -> ElectricField:
-        """pad -> ft2 -> x H -> ift2 -> crop (Props/ASM_Prop.py:314-378), on the MI355X kernels."""
+        """pad -> ft2 -> x H -> ift2 -> crop (Props/ASM_Prop.py:314-378), on the MI355X kernels.
+        Inside propagation.deferred_output() the returned field carries the propagation unevaluated
+        (_PendingAsm) so the QAT loss can be folded into it."""
+        if _prop.deferring():
+            B, C, H, W = field.shape
+            if not (self.do_padding and not self.do_unpad_after_pad):
+                Ho, Wo = H, W
+            else:
+                ph, pw = self.compute_padding(H, W, return_size_of_padding=True)
+                Ho, Wo = H + 2 * ph, W + 2 * pw
+            holder = torch.zeros((), dtype=torch.complex64, device=field.device).expand(B, C, Ho, Wo)
+            Eout = ElectricField(data=holder, wavelengths=field.wavelengths, spacing=field.spacing,
+                                 device=field.device)._adopt_host(field)
+            Eout._pending = _PendingAsm(self, field, self._zh[:1])
+            return Eout
         out = self._run(field, self._zh[:1])
         Eout = ElectricField(data=out[0], wavelengths=field.wavelengths, spacing=field.spacing, device=field.device)
         return Eout._adopt_host(field)

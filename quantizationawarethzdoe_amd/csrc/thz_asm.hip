@@ -56,6 +56,11 @@ struct AsmArgs {
   float* mod_hfull;     // optional: the noisy, upsampled height map [Hin][Win]
   int mod_hs, mod_ws;
   float mod_tol, mod_eps, mod_tand;
+  // fused |E|^2 -> normalize -> MSE in K3's storer (thz_asm_forward_loss, Z == 1): ls.stats
+  // non-null; K1 zeroes its accumulators
+  LossSink ls;
+  // mixed-radix K2 tables of the first z-chunk computed by tab_blocks extra K1 workgroups
+  int tab_blocks;
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
@@ -167,12 +172,24 @@ __device__ __forceinline__ float2 vrs_ez(float2 ex, float2 ey, float x, float y,
 #pragma clang fp contract(on)
 
 template <int PN>
+__device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq);
+
+template <int PN>
 __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
                                                     FftPlan pw, AsmArgs a) {
   extern __shared__ float2 lds[];
-  const int row = xcd_rows(blockIdx.x, gridDim.x);
-  const int bc = row / a.Hin, h = row - bc * a.Hin;
   const int tid = threadIdx.x, nt = blockDim.x;
+  const int nrows = gridDim.x - a.tab_blocks;
+  if constexpr (is_mx(PN)) {
+    // the extra workgroups past the rows: the mixed-radix column pass's tables of the first
+    // z-chunk (asm_tf_tables, one launch fewer; K2 runs after this kernel on the stream)
+    if ((int)blockIdx.x >= nrows) {
+      tf_tables_body<PN>(a, blockIdx.x - nrows, 1);
+      return;
+    }
+  }
+  const int row = xcd_rows(blockIdx.x, nrows);
+  const int bc = row / a.Hin, h = row - bc * a.Hin;
   const float2* src = in + ((size_t)bc * a.Hin + h) * a.Win;
   float2* dst = T + (size_t)bc * a.ncb * CB * a.Hin;
   // VRS (Props/RSC_Prop.py:294-303): plane b = 2 is Ez = Ex x / r + Ey y / r on the unpadded
@@ -400,8 +417,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
 // chunk (bisection with the exact reference-order tests, one lane per z; see asm_cols).  Every
 // plane of the wavelength shares them, so the column pass does no fp32 division.
 template <int PN>
-__global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
-  const int li = blockIdx.x / a.ncols, c = blockIdx.x - li * a.ncols;
+__device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq) {
+  const int li = blk / a.ncols, c = blk - li * a.ncols;
   const float lam = a.lam[li];
   const float Ky = kfreq(c - a.J, a.Pw, a.dy);
   const size_t col = (size_t)li * a.ncols + c;
@@ -443,6 +460,11 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
     }
     a.mzt[col * a.nz + zz] = lo;
   }
+}
+
+template <int PN>
+__global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
+  tf_tables_body<PN>(a, blockIdx.x, with_sq);
 }
 
 // K2 for a compile-time mixed-radix Ph (MxPlan, blockDim MX_T): the power-of-two kernel's
@@ -528,15 +550,32 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
 // ---------------------------------------------------------------------------------------------
 // K3: per output row: gather band from U, IFFT(Pw), crop -> out[z][bc][r][w]
 // ---------------------------------------------------------------------------------------------
-template <int PN>
-__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* __restrict__ U, float2* __restrict__ out,
-                                                    FftPlan pw, AsmArgs a) {
+// LOSS: the stored row also feeds the |E|^2 -> normalize -> MSE sums of its batch item
+// (LossAcc; Z == 1 so plane == bc), stored per workgroup in slot (c, r) of b by loss_store_part.
+template <int PN, bool LOSS>
+__device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw,
+                                              const AsmArgs& a) {
   extern __shared__ float2 lds[];
   const int row = xcd_rows(blockIdx.x, gridDim.x);  // row in [0, nz*BC*Hout)
   const int plane = row / a.Hout, r = row - plane * a.Hout;  // plane = zz*BC + bc
   const int tid = threadIdx.x, nt = blockDim.x;
   const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
+  LossAcc acc;
+  const float* trow = nullptr;
+  unsigned ibase = 0;
+  int lb = 0, lc = 0;
+  if constexpr (LOSS) {
+    lb = plane / a.C;
+    lc = plane - lb * a.C;
+    const int tb = a.ls.tB == 1 ? 0 : lb, tc = a.ls.tC == 1 ? 0 : lc;
+    trow = a.ls.target + (((size_t)tb * a.ls.tC + tc) * a.Hout + r) * a.Wout;
+    ibase = (unsigned)((lc * a.Hout + r) * a.Wout);
+  }
+  auto put = [&](int w, float2 v) {
+    dst[w] = v;
+    if constexpr (LOSS) acc.add(v, trow[w], ibase + (unsigned)w);
+  };
   if constexpr (is_mx(PN)) {
     const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
     auto ld = [&](int, int, int j) {
@@ -545,7 +584,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int w = j - a.out_c0;
-      if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
+      if ((unsigned)w < (unsigned)a.Wout) put(w, v);
     };
     Mx300::run<true, MX_T>(lds, twr, tid, ld, sv);
   } else if constexpr (PN > 0) {
@@ -572,7 +611,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int w = j - a.out_c0;
-      if ((unsigned)w < (unsigned)a.Wout) dst[w] = v;
+      if ((unsigned)w < (unsigned)a.Wout) put(w, v);
     };
     fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
   } else {
@@ -582,8 +621,21 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* 
     }
     __syncthreads();
     fft_lds<true>(lds, pw, tid, nt);
-    for (int w = tid; w < a.Wout; w += nt) dst[w] = lds[padx(a.out_c0 + w)];
+    for (int w = tid; w < a.Wout; w += nt) put(w, lds[padx(a.out_c0 + w)]);
   }
+  if constexpr (LOSS) loss_store_part(acc, a.ls, lb, lc * a.Hout + r);  // C Hout slots per b
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* __restrict__ U, float2* __restrict__ out,
+                                                    FftPlan pw, AsmArgs a) {
+  rows_inv_body<PN, false>(U, out, pw, a);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv_loss(const float2* __restrict__ U,
+                                                                       float2* __restrict__ out, FftPlan pw, AsmArgs a) {
+  rows_inv_body<PN, true>(U, out, pw, a);
 }
 
 
@@ -784,6 +836,7 @@ static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_rows_fwd<PN>);
   ks.push_back((const void*)asm_cols<PN>);
   ks.push_back((const void*)asm_rows_inv<PN>);
+  ks.push_back((const void*)asm_rows_inv_loss<PN>);
   ks.push_back((const void*)fft_rows_kernel<PN>);
   ks.push_back((const void*)rsc_k_rows<PN>);
   ks.push_back((const void*)rsc_k_cols<PN>);
@@ -887,9 +940,14 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     a.sqt = (float*)tabs;
     a.mzt = (int*)(tabs + tab_sq_bytes(g));
   }
+  // square mixed-radix grids (cfg4 / cfg5): the first z-chunk's column tables ride along with K1
+  a.tab_blocks = mx_tabs && mx_kind(g.Pw) == Mx300::N ? g.C * g.ncols : 0;
   {
     KernelTimer kt("asm_rows_fwd", s);
-    THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in, T, pw, a);
+    a.zoff = 0;
+    a.nz = std::min(g.zc, Z);
+    THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin + a.tab_blocks), fft_lds_bytes_io(g.Pw), s,
+                    (const float2*)in, T, pw, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
@@ -899,7 +957,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     {
       KernelTimer kt("asm_cols", s);
       if (mx_kind(g.Ph) == Mx300::N) {
-        if (mx_tabs) {
+        if (mx_tabs && !(z0 == 0 && a.tab_blocks)) {
           hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
           THZ_LAUNCH_CHECK();
         }
@@ -918,8 +976,15 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     }
     {
       KernelTimer kt("asm_rows_inv", s);
-      THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
-                      (float2*)out, pw, a);
+      if (a.ls.stats) {
+        THZ_ROWS_SWITCH(g.Pw, asm_rows_inv_loss, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s,
+                        (const float2*)U, (float2*)out, pw, a);
+        THZ_LAUNCH_CHECK();
+        if ((e = launch_loss_finish(a.ls, s))) return e;
+      } else {
+        THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
+                        (float2*)out, pw, a);
+      }
       THZ_LAUNCH_CHECK();
       kt.stop();
     }
@@ -954,7 +1019,7 @@ extern "C" int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes) {
 namespace thz {
 static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const float* mh, const float* mu,
                             float* mhfull, const void* in, void* out, void* workspace, size_t workspace_bytes,
-                            thz_stream_t stream) {
+                            thz_stream_t stream, const LossSink* ls = nullptr) {
   int e = validate(d);
   if (e) return e;
   if (!in || !out) return fail(THZ_E_ARG, "null data pointer");
@@ -1002,6 +1067,7 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
     a.mod_eps = m->epsilon;
     a.mod_tand = m->tand;
   }
+  if (ls) a.ls = *ls;
 
   float2* T = (float2*)workspace;
   float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
@@ -1025,6 +1091,32 @@ extern "C" int thz_asm_forward_modulated(const thz_asm_desc* d, const thz_doe_de
                 d->B, d->C, d->H, d->W);
   if (m->hs < 1 || m->ws < 1) return fail(THZ_E_ARG, "bad height-map size %dx%d", m->hs, m->ws);
   return asm_forward_impl(d, m, height, noise, height_full, field, out, workspace, workspace_bytes, stream);
+}
+
+extern "C" int thz_asm_forward_loss(const thz_asm_desc* d, const thz_doe_desc* m, const void* field,
+                                    const float* height, const float* noise, float* height_full,
+                                    const thz_loss_desc* l, const float* target, void* out, float* loss, float* stats,
+                                    void* workspace, size_t workspace_bytes, thz_stream_t stream) {
+  int e = validate(d);
+  if (e) return e;
+  if (!l || !target || !loss || !stats) return fail(THZ_E_ARG, "null loss descriptor / target / loss / stats");
+  if (d->adjoint || d->Z != 1) return fail(THZ_E_ARG, "the fused loss takes one forward z-plane (Z = %d)", d->Z);
+  const int Ho = d->unpad ? d->H : d->H + 2 * d->pad_h, Wo = d->unpad ? d->W : d->W + 2 * d->pad_w;
+  if (l->B != d->B || l->C != d->C || l->H != Ho || l->W != Wo)
+    return fail(THZ_E_ARG, "loss field %dx%dx%dx%d does not match the ASM output %dx%dx%dx%d", l->B, l->C, l->H, l->W,
+                d->B, d->C, Ho, Wo);
+  if (!(l->tB == 1 || l->tB == l->B) || !(l->tC == 1 || l->tC == l->C))
+    return fail(THZ_E_ARG, "target %dx%d does not broadcast over %dx%d", l->tB, l->tC, l->B, l->C);
+  if (m) {
+    if (!height) return fail(THZ_E_ARG, "null height map");
+    if (m->B != d->B || m->C != d->C || m->H != d->H || m->W != d->W)
+      return fail(THZ_E_ARG, "DOE field %dx%dx%dx%d does not match the ASM input %dx%dx%dx%d", m->B, m->C, m->H,
+                  m->W, d->B, d->C, d->H, d->W);
+    if (m->hs < 1 || m->ws < 1) return fail(THZ_E_ARG, "bad height-map size %dx%d", m->hs, m->ws);
+  }
+  const LossSink ls = loss_sink(l, target, loss, stats, l->C * l->H);
+  return asm_forward_impl(d, m, m ? height : nullptr, m ? noise : nullptr, m ? height_full : nullptr, field, out,
+                          workspace, workspace_bytes, stream, &ls);
 }
 
 namespace thz {

@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "../../include/thzdoe.h"
+
 namespace thz {
 
 // Blocks b and b+8 share an XCD (MI355X_MICROARCH.md §Workgroup dispatch).  Map each run
@@ -197,5 +199,118 @@ __device__ __forceinline__ float2 doe_transmission(float hv, float lam, float ep
   return make_float2(loss * cs, loss * sn);
 }
 #pragma clang fp contract(on)
+
+// ---------------------------------------------------------------------------------------------
+// |E|^2 -> normalize -> MSE as one-pass sums (experiment_four_focal_spots.ipynb:336-370,
+// utils/Helper_Functions.py:185-193).  With m_b = max_i I_i of batch item b,
+//   sum_i (I_i / m_b - T_i)^2 = S_II / m_b^2 - 2 S_IT / m_b + S_TT,
+// so one pass accumulating S_II, S_IT, S_TT (fp64) and the max key per b replaces the two passes
+// (max, then residuals) of a direct restatement.  The max key is (fp32 bits of I) << 32 |
+// (0xffffffff - index): I >= 0 orders as its bits, ties go to the first index (torch.max).
+// The backward statistic S_b = sum_i r_i I_i (r_i = I_i / m_b - T_i) is S_II / m_b - S_IT.
+//
+// Each producing workgroup stores its partial sums in its own slot (no atomics: a device-scope
+// atomic per workgroup serialises a large batch on a few memory-side lines); loss_finish_kernel
+// (thz_optics.hip) reduces the per_b slots of each b in a fixed order and the last of its
+// workgroups sums the B terms, so the loss is bitwise reproducible.  Stats buffer layout
+// (thz_intensity_mse_workspace_size): floats [0, 3B) = {m, argmax bits, S} per b; at byte 16 B:
+// LossPart [B][per_b]; fp64 terms [B]; u64 finished-workgroup counter (zeroed by the producer).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float loss_intensity(float2 e) {
+  const float m = hypotf(e.x, e.y);  // torch.abs(E) ** 2
+  return m * m;
+}
+
+struct LossPart {
+  double ii, it, tt;
+  unsigned long long key;
+};
+
+struct LossAcc {
+  double ii = 0.0, it = 0.0, tt = 0.0;
+  unsigned long long key = 0ull;
+  __device__ __forceinline__ void add(float2 v, float t, unsigned idx) {
+    const float I = loss_intensity(v);
+    const double di = I, dt = t;
+    ii = fma(di, di, ii);
+    it = fma(di, dt, it);
+    tt = fma(dt, dt, tt);
+    const unsigned long long k = ((unsigned long long)__float_as_uint(I) << 32) | (0xffffffffu - idx);
+    key = k > key ? k : key;
+  }
+  __device__ __forceinline__ static LossAcc of(const LossPart& p) {
+    LossAcc a;
+    a.ii = p.ii;
+    a.it = p.it;
+    a.tt = p.tt;
+    a.key = p.key;
+    return a;
+  }
+  __device__ __forceinline__ LossPart part() const { return LossPart{ii, it, tt, key}; }
+  __device__ __forceinline__ void merge(const LossAcc& o) {
+    ii += o.ii;
+    it += o.it;
+    tt += o.tt;
+    key = o.key > key ? o.key : key;
+  }
+};
+
+struct LossSink {
+  const float* target;        // [tB][tC][H][W]
+  float* loss;                // [1]
+  float* stats;               // [B][3] + the slots above
+  int B, tB, tC;
+  int per_b;                  // producer slots per batch item
+  double inv_n;               // 1 / (B C H W)
+  __host__ __device__ static size_t part_offset(int B) { return 16 * (size_t)B; }  // bytes
+  __host__ __device__ static size_t bytes(int B, int per_b) {
+    return part_offset(B) + sizeof(LossPart) * (size_t)B * per_b + 8 * (size_t)B + 8;
+  }
+  __device__ LossPart* parts() const { return (LossPart*)((char*)stats + part_offset(B)); }
+  __device__ double* terms() const { return (double*)(parts() + (size_t)B * per_b); }
+  __device__ unsigned long long* counter() const { return (unsigned long long*)(terms() + B); }
+};
+
+inline LossSink loss_sink(const thz_loss_desc* d, const float* target, float* loss, float* stats, int per_b) {
+  LossSink ls;
+  ls.target = target;
+  ls.loss = loss;
+  ls.stats = stats;
+  ls.B = d->B;
+  ls.tB = d->tB;
+  ls.tC = d->tC;
+  ls.per_b = per_b;
+  ls.inv_n = 1.0 / ((double)d->B * d->C * d->H * d->W);
+  return ls;
+}
+
+// Workgroup reduction of the accumulators (fixed order), stored by thread 0 in slot (b, slot).
+// Workgroup (0, 0) also zeroes the finish kernel's counter (it runs after this launch).
+__device__ __forceinline__ void loss_store_part(LossAcc acc, const LossSink& ls, int b, int slot) {
+  __shared__ LossPart s_a[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  for (int o = 32; o > 0; o >>= 1) {
+    LossAcc t;
+    t.ii = __shfl_xor(acc.ii, o);
+    t.it = __shfl_xor(acc.it, o);
+    t.tt = __shfl_xor(acc.tt, o);
+    t.key = __shfl_xor(acc.key, o);
+    acc.merge(t);
+  }
+  if (nw > 1) {
+    __syncthreads();
+    if (lane == 0) s_a[wid] = acc.part();
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int w = 1; w < nw; ++w) acc.merge(LossAcc::of(s_a[w]));
+  }
+  if (threadIdx.x == 0) {
+    ls.parts()[(size_t)b * ls.per_b + slot] = LossPart{acc.ii, acc.it, acc.tt, acc.key};
+    if (blockIdx.x == 0 && blockIdx.y == 0) *ls.counter() = 0ull;
+  }
+}
+
+// loss_finish_kernel launch (thz_optics.hip): B workgroups
+int launch_loss_finish(const LossSink& ls, hipStream_t s);
 
 }  // namespace thz

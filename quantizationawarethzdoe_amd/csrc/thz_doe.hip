@@ -132,6 +132,10 @@ struct QArgs {
   float plut_w[THZ_MAX_LUT];  // wrapped phase LUT (SGV3)
 };
 
+// Loops over the LUT levels run to the compile-time bound with a guard, so the per-level arrays
+// (logits, Gumbel draws, y) stay in registers instead of dynamically indexed scratch memory.
+#define THZ_FOR_LEVELS(l, n) _Pragma("unroll") for (int l = 0; l < THZ_MAX_LUT; ++l) if (l < (n))
+
 __device__ __forceinline__ float sigm(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 #pragma clang fp contract(off)
@@ -146,18 +150,18 @@ __device__ __forceinline__ float wrap_pi(float x) {
   return rem_pos(x + PI, TWO_PI) - PI;
 }
 // SGV3 scores (score_phase(func='sigmoid') * c_s * s, :794-817, :833) and d score / d phase
-__device__ __forceinline__ void sgv3_score(const QArgs& a, float phase, int l, float* score, float* dscore) {
+__device__ __forceinline__ void sgv3_score(const QArgs& a, float sv, float phase, int l, float* score, float* dscore) {
   const float PI = 3.1415927410125732f, TWO_PI = 6.2831854820251465f;
   const float wp = wrap_pi(phase);
   float d = wp - a.plut_w[l];
   d = rem_pos(d + PI, TWO_PI) - PI;
   d = d / PI;
-  const float z = a.s * d;
+  const float z = sv * d;
   const float sg = sigm(z);
   const float sc = sg * (1.0f - sg) * 4.0f;
-  *score = (sc * a.c_s) * a.s;
+  *score = (sc * a.c_s) * sv;
   // d/dphase: 4 sg (1-sg)(1-2sg) * s/pi * c_s * s
-  *dscore = 4.0f * sg * (1.0f - sg) * (1.0f - 2.0f * sg) * (a.s / PI) * a.c_s * a.s;
+  *dscore = 4.0f * sg * (1.0f - sg) * (1.0f - 2.0f * sg) * (sv / PI) * a.c_s * sv;
 }
 
 // quadrant pixel (i, j) -> its up to four mirror positions in the full map (:28-35)
@@ -179,18 +183,18 @@ __device__ __forceinline__ void for_mirrors(const QArgs& a, int i, int j, F fn) 
 // gumbel_softmax(logits, tau, hard) over L values: returns the hard index, y_soft in y
 __device__ __forceinline__ int gumbel_soft(const float* logits, const float* expo, int L, float tau, float* y) {
   float mx = -INFINITY;
-  for (int l = 0; l < L; ++l) {
+  THZ_FOR_LEVELS(l, L) {
     y[l] = (logits[l] + (-logf(expo[l]))) / tau;
     mx = fmaxf(mx, y[l]);
   }
   float sum = 0.f;
-  for (int l = 0; l < L; ++l) {
+  THZ_FOR_LEVELS(l, L) {
     y[l] = expf(y[l] - mx);
     sum += y[l];
   }
   int arg = 0;
   float best = -1.f;
-  for (int l = 0; l < L; ++l) {
+  THZ_FOR_LEVELS(l, L) {
     y[l] = y[l] / sum;
     if (y[l] > best) {
       best = y[l];
@@ -203,21 +207,22 @@ __device__ __forceinline__ int gumbel_soft(const float* logits, const float* exp
 // straight-through value sum_l lut_l * ((onehot_l - y_l) + y_l)
 __device__ __forceinline__ float st_value(const QArgs& a, const float* y, int arg) {
   float q = 0.f;
-  for (int l = 0; l < a.L; ++l) q += a.lut[l] * (((l == arg ? 1.0f : 0.0f) - y[l]) + y[l]);
+  THZ_FOR_LEVELS(l, a.L) q += a.lut[l] * (((l == arg ? 1.0f : 0.0f) - y[l]) + y[l]);
   return q;
 }
 
-__device__ __forceinline__ void apply_dyn(QArgs& a) {
-  if (a.dyn) {
-    a.tau = a.dyn[0];
-    a.s = a.dyn[1];
-    a.beta = a.dyn[2];
-  }
+// the schedule values of this launch: the descriptor's, or the graph-replay device buffer's.
+// The kernels keep QArgs unmodified (a written by-value struct is copied to scratch memory).
+struct QDyn {
+  float tau, s, beta;
+};
+__device__ __forceinline__ QDyn get_dyn(const QArgs& a) {
+  return a.dyn ? QDyn{a.dyn[0], a.dyn[1], a.dyn[2]} : QDyn{a.tau, a.s, a.beta};
 }
 
 __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __restrict__ expo,
                           float* __restrict__ hfull, float* __restrict__ ysave) {
-  apply_dyn(a);
+  const QDyn q = get_dyn(a);
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = a.hq * a.wq;
   if (p >= n) return;
@@ -225,20 +230,20 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
   float out;
   float y[THZ_MAX_LUT];
   if (a.kind == THZ_Q_NGS) {
-    const int arg = gumbel_soft(w + (size_t)p * a.L, expo + (size_t)p * a.L, a.L, a.tau, y);
+    const int arg = gumbel_soft(w + (size_t)p * a.L, expo + (size_t)p * a.L, a.L, q.tau, y);
     out = st_value(a, y, arg);
-    for (int l = 0; l < a.L; ++l) ysave[(size_t)p * a.L + l] = y[l];
+    THZ_FOR_LEVELS(l, a.L) ysave[(size_t)p * a.L + l] = y[l];
   } else if (a.kind == THZ_Q_SGV1) {
     // the weight is the phase itself (:411-445): scores of w, Gumbel pick, LUT value
     float logits[THZ_MAX_LUT], ex[THZ_MAX_LUT];
-    for (int l = 0; l < a.L; ++l) {
+    THZ_FOR_LEVELS(l, a.L) {
       float dsc;
-      sgv3_score(a, w[p], l, &logits[l], &dsc);
+      sgv3_score(a, q.s, w[p], l, &logits[l], &dsc);
       ex[l] = expo[(size_t)l * n + p];
     }
-    const int arg = gumbel_soft(logits, ex, a.L, a.tau, y);
+    const int arg = gumbel_soft(logits, ex, a.L, q.tau, y);
     out = st_value(a, y, arg);
-    for (int l = 0; l < a.L; ++l) ysave[(size_t)l * n + p] = y[l];
+    THZ_FOR_LEVELS(l, a.L) ysave[(size_t)l * n + p] = y[l];
   } else {
     const float wc = fminf(fmaxf(w[p], -a.clampv), a.clampv);
     const float hm = a.hmax * sigm(wc);
@@ -246,7 +251,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
     if (a.kind == THZ_Q_STE) {
       int arg = 0;
       float best = INFINITY;
-      for (int l = 0; l < a.L; ++l) {
+      THZ_FOR_LEVELS(l, a.L) {
         const float dd = fabsf(hm - a.lut[l]);
         if (dd < best) {
           best = dd;
@@ -258,20 +263,20 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
       const float delta = (a.hmax - 0.0f) / (float)(a.L - 1);
       const float xn = (hm - 0.0f) / delta - 0.5f;
       float sm = 0.f;
-      for (int l = 0; l < a.L - 1; ++l) sm += sigm(a.tau * (xn - (float)l));
+      THZ_FOR_LEVELS(l, a.L - 1) sm += sigm(q.tau * (xn - (float)l));
       out = 0.0f + delta * sm;
     } else if (a.kind == THZ_Q_SGV3 && a.iter_frac > 0.3f) {
       const float phase = a.phase_scale * hm;
       float logits[THZ_MAX_LUT], ex[THZ_MAX_LUT];
-      for (int l = 0; l < a.L; ++l) {
+      THZ_FOR_LEVELS(l, a.L) {
         float dsc;
-        sgv3_score(a, phase, l, &logits[l], &dsc);
+        sgv3_score(a, q.s, phase, l, &logits[l], &dsc);
         ex[l] = expo[(size_t)l * n + p];
       }
-      const int arg = gumbel_soft(logits, ex, a.L, a.tau, y);
-      const float q = st_value(a, y, arg);
-      out = a.iter_frac <= 0.8f ? (1.0f - a.beta) * hm + a.beta * q : q;
-      for (int l = 0; l < a.L; ++l) ysave[(size_t)l * n + p] = y[l];
+      const int arg = gumbel_soft(logits, ex, a.L, q.tau, y);
+      const float qv = st_value(a, y, arg);
+      out = a.iter_frac <= 0.8f ? (1.0f - q.beta) * hm + q.beta * qv : qv;
+      THZ_FOR_LEVELS(l, a.L) ysave[(size_t)l * n + p] = y[l];
     }
   }
   for_mirrors(a, i, j, [&](int o) { hfull[o] = out; });
@@ -279,7 +284,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
 
 __global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __restrict__ ysave,
                           const float* __restrict__ gfull, float* __restrict__ gw) {
-  apply_dyn(a);
+  const QDyn q = get_dyn(a);
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int n = a.hq * a.wq;
   if (p >= n) return;
@@ -289,22 +294,22 @@ __global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __r
   if (a.kind == THZ_Q_NGS) {
     // d logits_l = y_l (dy_l - sum_k y_k dy_k) / tau, dy_l = G lut_l
     float dot = 0.f;
-    for (int l = 0; l < a.L; ++l) dot += ysave[(size_t)p * a.L + l] * G * a.lut[l];
-    for (int l = 0; l < a.L; ++l) {
+    THZ_FOR_LEVELS(l, a.L) dot += ysave[(size_t)p * a.L + l] * G * a.lut[l];
+    THZ_FOR_LEVELS(l, a.L) {
       const float yl = ysave[(size_t)p * a.L + l];
-      gw[(size_t)p * a.L + l] = yl * (G * a.lut[l] - dot) / a.tau;
+      gw[(size_t)p * a.L + l] = yl * (G * a.lut[l] - dot) / q.tau;
     }
     return;
   }
   if (a.kind == THZ_Q_SGV1) {
     float dot = 0.f;
-    for (int l = 0; l < a.L; ++l) dot += ysave[(size_t)l * n + p] * G * a.lut[l];
+    THZ_FOR_LEVELS(l, a.L) dot += ysave[(size_t)l * n + p] * G * a.lut[l];
     float dphase = 0.f;
-    for (int l = 0; l < a.L; ++l) {
+    THZ_FOR_LEVELS(l, a.L) {
       const float yl = ysave[(size_t)l * n + p];
       float sc, dsc;
-      sgv3_score(a, w[p], l, &sc, &dsc);
-      dphase += yl * (G * a.lut[l] - dot) / a.tau * dsc;
+      sgv3_score(a, q.s, w[p], l, &sc, &dsc);
+      dphase += yl * (G * a.lut[l] - dot) / q.tau * dsc;
     }
     gw[p] = dphase;
     return;
@@ -318,26 +323,26 @@ __global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __r
     const float delta = (a.hmax - 0.0f) / (float)(a.L - 1);
     const float xn = (hm - 0.0f) / delta - 0.5f;
     float d = 0.f;
-    for (int l = 0; l < a.L - 1; ++l) {
-      const float s2 = sigm(a.tau * (xn - (float)l));
-      d += s2 * (1.0f - s2) * a.tau;
+    THZ_FOR_LEVELS(l, a.L - 1) {
+      const float s2 = sigm(q.tau * (xn - (float)l));
+      d += s2 * (1.0f - s2) * q.tau;
     }
     dhm = G * d;  // delta * sum(tau sig') / delta
   } else if (a.kind == THZ_Q_SGV3 && a.iter_frac > 0.3f) {
     const bool blend = a.iter_frac <= 0.8f;
-    const float gq = blend ? a.beta * G : G;
+    const float gq = blend ? q.beta * G : G;
     float dot = 0.f;
-    for (int l = 0; l < a.L; ++l) dot += ysave[(size_t)l * n + p] * gq * a.lut[l];
+    THZ_FOR_LEVELS(l, a.L) dot += ysave[(size_t)l * n + p] * gq * a.lut[l];
     const float phase = a.phase_scale * hm;
     float dphase = 0.f;
-    for (int l = 0; l < a.L; ++l) {
+    THZ_FOR_LEVELS(l, a.L) {
       const float yl = ysave[(size_t)l * n + p];
-      const float dlogit = yl * (gq * a.lut[l] - dot) / a.tau;
+      const float dlogit = yl * (gq * a.lut[l] - dot) / q.tau;
       float sc, dsc;
-      sgv3_score(a, phase, l, &sc, &dsc);
+      sgv3_score(a, q.s, phase, l, &sc, &dsc);
       dphase += dlogit * dsc;
     }
-    dhm = (blend ? (1.0f - a.beta) * G : 0.0f) + dphase * a.phase_scale;
+    dhm = (blend ? (1.0f - q.beta) * G : 0.0f) + dphase * a.phase_scale;
   }
   const bool inside = wv >= -a.clampv && wv <= a.clampv;  // clamp passes the gradient on [min, max]
   gw[p] = inside ? dhm * a.hmax * sg * (1.0f - sg) : 0.0f;

@@ -107,10 +107,13 @@ __global__ void aperture_kernel(const float2* __restrict__ in, float2* __restric
 }
 
 // ---------------------------------------------------------------------------------------------
-// |E|^2 -> normalize (per batch item, by its max) -> MSE against a broadcast target
-// stats[b] = {max, argmax (as float bits), sum_i r_i I_i} with r_i = I_i/m - T_i
+// |E|^2 -> normalize (per batch item, by its max) -> MSE against a broadcast target, as the
+// one-pass sums of thz_dev.hpp (LossAcc / loss_store_part): a grid of (chunks, B) workgroups, one
+// slot each, then loss_finish_kernel.  stats[b] = {max, argmax (as float bits), sum_i r_i I_i}, r_i = I_i/m - T_i.
+// (The ASM path folds the same accumulation into its row-inverse pass: thz_asm_forward_loss.)
 // ---------------------------------------------------------------------------------------------
-constexpr int LOSS_THREADS = 1024;
+constexpr int LOSS_THREADS = 256;
+constexpr int LOSS_PER_THREAD = 8;
 
 struct LossArgs {
   int B, C, H, W, tB, tC;
@@ -121,74 +124,85 @@ __device__ __forceinline__ float target_at(const float* t, const LossArgs& a, in
   return t[((size_t)tb * a.tC + tc) * a.H * a.W + p];
 }
 
-__device__ __forceinline__ float intensity(float2 e) {
-  // torch.abs(E) ** 2: |E| = hypot, then squared
-  const float m = hypotf(e.x, e.y);
-  return m * m;
-}
+__device__ __forceinline__ float intensity(float2 e) { return loss_intensity(e); }
 
-__global__ void __launch_bounds__(LOSS_THREADS) mse_forward_kernel(const float2* __restrict__ f,
-                                                                   const float* __restrict__ t,
-                                                                   float* __restrict__ partial,
-                                                                   float* __restrict__ stats, LossArgs a) {
-  __shared__ float s_v[LOSS_THREADS / 64];
-  __shared__ int s_i[LOSS_THREADS / 64];
-  __shared__ float s_a[LOSS_THREADS / 64], s_b[LOSS_THREADS / 64];
-  const int b = blockIdx.x;
+__global__ void __launch_bounds__(LOSS_THREADS) mse_forward_kernel(const float2* __restrict__ f, LossArgs a,
+                                                                   LossSink ls) {
+  const int b = blockIdx.y;
   const int HW = a.H * a.W, n = a.C * HW;
   const float2* fb = f + (size_t)b * n;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // pass 1: max and its first index
-  float mv = -1.f;
-  int mi = 0x7fffffff;
-  for (int i = threadIdx.x; i < n; i += LOSS_THREADS) {
-    const float v = intensity(fb[i]);
-    if (v > mv) { mv = v; mi = i; }
+  LossAcc acc;
+  const int i0 = blockIdx.x * LOSS_THREADS * LOSS_PER_THREAD + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < LOSS_PER_THREAD; ++k) {
+    const int i = i0 + k * LOSS_THREADS;
+    if (i < n) {
+      const int c = i / HW, p = i - c * HW;
+      acc.add(fb[i], target_at(ls.target, a, b, c, p), (unsigned)i);
+    }
+  }
+  loss_store_part(acc, ls, b, blockIdx.x);
+}
+
+// One workgroup per batch item: reduce its per_b slots (fixed order), write its statistics and
+// loss term; the last workgroup to finish sums the B terms in order into the loss.
+constexpr int FIN_THREADS = 256;
+__global__ void __launch_bounds__(FIN_THREADS) loss_finish_kernel(LossSink ls) {
+  __shared__ LossPart s_a[FIN_THREADS / 64];
+  __shared__ int s_last;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const LossPart* pp = ls.parts() + (size_t)b * ls.per_b;
+  LossAcc acc;
+  for (int q = threadIdx.x; q < ls.per_b; q += FIN_THREADS) {
+    const LossPart p = pp[q];
+    acc.merge(LossAcc::of(p));
   }
   for (int o = 32; o > 0; o >>= 1) {
-    const float ov = __shfl_xor(mv, o);
-    const int oi = __shfl_xor(mi, o);
-    if (ov > mv || (ov == mv && oi < mi)) { mv = ov; mi = oi; }
+    LossAcc t;
+    t.ii = __shfl_xor(acc.ii, o);
+    t.it = __shfl_xor(acc.it, o);
+    t.tt = __shfl_xor(acc.tt, o);
+    t.key = __shfl_xor(acc.key, o);
+    acc.merge(t);
   }
-  if (lane == 0) { s_v[wid] = mv; s_i[wid] = mi; }
+  if (lane == 0) s_a[wid] = acc.part();
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < LOSS_THREADS / 64; ++w)
-      if (s_v[w] > s_v[0] || (s_v[w] == s_v[0] && s_i[w] < s_i[0])) { s_v[0] = s_v[w]; s_i[0] = s_i[w]; }
+    for (int w = 1; w < FIN_THREADS / 64; ++w) acc.merge(LossAcc::of(s_a[w]));
+    const float m = __uint_as_float((unsigned)(acc.key >> 32));
+    const double md = m;
+    ls.stats[3 * b + 0] = m;
+    ls.stats[3 * b + 1] = __int_as_float((int)(0xffffffffu - (unsigned)acc.key));
+    ls.stats[3 * b + 2] = (float)(acc.ii / md - acc.it);
+    ls.terms()[b] = acc.ii / (md * md) - 2.0 * acc.it / md + acc.tt;
+    __threadfence();
+    s_last = atomicAdd(ls.counter(), 1ull) == (unsigned long long)(ls.B - 1);
   }
   __syncthreads();
-  const float m = s_v[0];
-  // pass 2: sum (I/m - T)^2 and sum (I/m - T) I
-  float se = 0.f, sr = 0.f;
-  for (int i = threadIdx.x; i < n; i += LOSS_THREADS) {
-    const int c = i / HW, p = i - c * HW;
-    const float I = intensity(fb[i]);
-    const float r = I / m - target_at(t, a, b, c, p);
-    se += r * r;
-    sr += r * I;
+  if (!s_last) return;
+  __threadfence();
+  double part = 0.0;  // B terms in order: thread t sums a contiguous run
+  const int per = (ls.B + FIN_THREADS - 1) / FIN_THREADS;
+  for (int q = threadIdx.x * per; q < min(ls.B, (threadIdx.x + 1) * per); ++q)
+    part += __hip_atomic_load(ls.terms() + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int o = 1; o < 64; o <<= 1) {  // ordered tree over the lanes
+    const double t = __shfl_down(part, o);
+    if ((lane & (2 * o - 1)) == 0 && lane + o < 64) part += t;
   }
-  for (int o = 32; o > 0; o >>= 1) {
-    se += __shfl_xor(se, o);
-    sr += __shfl_xor(sr, o);
-  }
-  if (lane == 0) { s_a[wid] = se; s_b[wid] = sr; }
+  __syncthreads();
+  if (lane == 0) s_a[wid].ii = part;
   __syncthreads();
   if (threadIdx.x == 0) {
-    float A = 0.f, Bv = 0.f;
-    for (int w = 0; w < LOSS_THREADS / 64; ++w) { A += s_a[w]; Bv += s_b[w]; }
-    partial[b] = A;
-    stats[3 * b + 0] = m;
-    stats[3 * b + 1] = __int_as_float(s_i[0]);
-    stats[3 * b + 2] = Bv;
+    double tot = 0.0;
+    for (int w = 0; w < FIN_THREADS / 64; ++w) tot += s_a[w].ii;
+    ls.loss[0] = (float)(tot * ls.inv_n);
   }
 }
 
-__global__ void mse_finish_kernel(const float* __restrict__ partial, float* __restrict__ loss, int B, float inv_n) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += partial[b];
-    loss[0] = s * inv_n;
-  }
+int launch_loss_finish(const LossSink& ls, hipStream_t s) {
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(ls.B), dim3(FIN_THREADS), 0, s, ls);
+  THZ_LAUNCH_CHECK();
+  return THZ_OK;
 }
 
 // dL/dE = 2 E dL/dI;  dL/dI_j = g (r_j / m - [j == argmax] sum_i r_i I_i / m^2),  g = 2 grad / N
@@ -419,7 +433,10 @@ extern "C" int thz_aperture(const thz_aperture_desc* d, const void* in, void* ou
 }
 
 extern "C" size_t thz_intensity_mse_workspace_size(const thz_loss_desc* d) {
-  return d && d->B > 0 ? sizeof(float) * 4 * (size_t)d->B : 0;
+  if (!d || d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1) return 0;
+  // slots per b: the loss kernel's chunks or the fused ASM row pass's C H rows, whichever is more
+  const size_t n = (size_t)d->C * d->H * d->W, per = LOSS_THREADS * LOSS_PER_THREAD;
+  return LossSink::bytes(d->B, (int)std::max((n + per - 1) / per, (size_t)d->C * d->H));
 }
 
 extern "C" int thz_intensity_mse_forward(const thz_loss_desc* d, const void* field, const float* target, float* loss,
@@ -428,13 +445,12 @@ extern "C" int thz_intensity_mse_forward(const thz_loss_desc* d, const void* fie
   if (!loss_args(d, &a) || !field || !target || !loss || !stats) return fail(THZ_E_ARG, "bad loss arguments");
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("intensity_mse_fwd", s);
-  float* partial = stats + 3 * (size_t)d->B;
-  hipLaunchKernelGGL(mse_forward_kernel, dim3(d->B), dim3(LOSS_THREADS), 0, s, (const float2*)field, target, partial,
-                     stats, a);
+  const int n = d->C * d->H * d->W, per = LOSS_THREADS * LOSS_PER_THREAD, chunks = (n + per - 1) / per;
+  const LossSink ls = loss_sink(d, target, loss, stats, chunks);
+  hipLaunchKernelGGL(mse_forward_kernel, dim3(chunks, d->B), dim3(LOSS_THREADS), 0, s, (const float2*)field, a, ls);
   THZ_LAUNCH_CHECK();
-  const double n = (double)d->B * d->C * d->H * d->W;
-  hipLaunchKernelGGL(mse_finish_kernel, dim3(1), dim3(64), 0, s, partial, loss, d->B, (float)(1.0 / n));
-  THZ_LAUNCH_CHECK();
+  int e = launch_loss_finish(ls, s);
+  if (e) return e;
   kt.stop();
   return THZ_OK;
 }

@@ -93,6 +93,7 @@ class PendingModulation:
     ASM_prop, inside its row pass (thz_asm_forward_modulated: the modulated field never goes to
     memory), or by ``run()`` -- the plain modulate kernel -- the first time anything reads the
     field's data.  ``hfull`` is the noisy upsampled height map, set by whichever runs first."""
+    kind = "modulation"
 
     def __init__(self, field, height, wavelengths, eps, tand, tolerance=None, noise=None):
         self.field, self.noise, self.tol = _modulate_args(field, height, tolerance, noise)

@@ -23,6 +23,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from quantizationawarethzdoe_amd import optics as _optics
+from quantizationawarethzdoe_amd import propagation as _prop
 from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
 from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
 from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
@@ -158,9 +160,11 @@ class DONNTrainer:
                 d._dyn = self.dyn
 
     def _loss(self, u, target, frac):
-        if self.loss_fn is None:
-            from quantizationawarethzdoe_amd.optics import intensity_mse
-            self.loss_fn = intensity_mse
+        if self.loss_fn is None or self.loss_fn is _optics.intensity_mse:
+            # the default loss folded into the detector propagation
+            with _prop.deferred_output():
+                out = self.model(u, frac, chained=self.chained)
+            return _optics.field_intensity_mse(out, target)
         out = self.model(u, frac, chained=self.chained)
         return self.loss_fn(out.data, target)
 

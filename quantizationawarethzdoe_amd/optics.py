@@ -152,6 +152,19 @@ def intensity_mse(field, target):
     return _IntensityMSE.apply(field, target)
 
 
+def field_intensity_mse(field, target):
+    """intensity_mse of an ElectricField.  When the field is the deferred output of an ASM_prop
+    (propagation.deferred_output), the loss is folded into that propagation's row-inverse pass
+    (thz_asm_forward_loss) and the field's data is set from the same pipeline; otherwise this is
+    intensity_mse(field.data, target)."""
+    pend = field._take_pending_propagation()
+    if pend is not None:
+        data, loss = pend.run_loss(target)
+        field.data = data
+        return loss
+    return intensity_mse(field.data, target)
+
+
 class _Resample(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, Hout, Wout, dx_in, dy_in, dx_out, dy_out):

@@ -8,8 +8,10 @@ path: a CPU tensor is an error.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
+import threading
 
 import torch
 
@@ -190,6 +192,126 @@ def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=
     return _AsmModulatedFunction.apply(pend.field, pend.height, pend, list(map(float, wavelengths)),
                                        tuple(map(float, spacing)), list(map(float, zs)), int(pad_h), int(pad_w),
                                        bool(unpad), bl)
+
+
+class _AsmLossFunction(torch.autograd.Function):
+    """One z-plane of ASM (optionally of a pending DOE modulation) whose row-inverse pass also
+    accumulates the QAT loss mean((normalize(|E|^2) - target)^2) (thz_asm_forward_loss).
+    Outputs (out [1,B,C,Ho,Wo], loss []).  Backward: the loss gradient of the stored field
+    (thz_intensity_mse_backward, plus the out cotangent when out is used elsewhere), the ASM
+    adjoint, then the modulate backward when a modulation was fused."""
+
+    @staticmethod
+    def forward(ctx, field, height, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
+        ctx.set_materialize_grads(False)
+        _require_device(field, "ASM")
+        field = field.contiguous()
+        B, C, H, W = field.shape
+        Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
+        t4 = target.detach().float().contiguous()
+        t4 = t4.reshape((1,) * (4 - t4.dim()) + tuple(t4.shape))
+        if tuple(t4.shape[-2:]) != (Ho, Wo) or t4.shape[0] not in (1, B) or t4.shape[1] not in (1, C):
+            raise ValueError(f"target {tuple(target.shape)} does not broadcast to field {(B, C, Ho, Wo)}")
+        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False)
+        ld = _lib.LossDesc(B=B, C=C, H=Ho, W=Wo, tB=t4.shape[0], tC=t4.shape[1])
+        L = _lib.lib()
+        nbytes = ctypes.c_size_t(0)
+        _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+        dev = field.device
+        ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=dev)
+        out = torch.empty((1, B, C, Ho, Wo), dtype=torch.complex64, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        stats = torch.empty(L.thz_intensity_mse_workspace_size(ctypes.byref(ld)) // 4, dtype=torch.float32,
+                            device=dev)
+        h = hfull = noise = None
+        m = None
+        if pend is not None:
+            h = height.detach().contiguous().float()
+            hfull = torch.empty((H, W), dtype=torch.float32, device=dev)
+            noise = pend.noise
+            m = pend.desc()
+
+        def ptr(t):
+            return ctypes.c_void_p(t.data_ptr() if t is not None else 0)
+
+        with torch.cuda.device(dev):
+            _lib.check(L.thz_asm_forward_loss(
+                ctypes.byref(d), ctypes.byref(m) if m is not None else None, ptr(field), ptr(h), ptr(noise),
+                ptr(hfull), ctypes.byref(ld), ptr(t4), ptr(out), ptr(loss), ptr(stats), ptr(ws),
+                ctypes.c_size_t(ws.numel()), _stream_handle()))
+        if pend is not None and pend.hfull is None:
+            pend.hfull = hfull
+        ctx.save_for_backward(field, h, out, t4, stats)
+        ctx.pend = pend
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit)
+        ctx.ldesc = (B, C, Ho, Wo, t4.shape[0], t4.shape[1])
+        return out, loss
+
+    @staticmethod
+    def backward(ctx, g_out, g_loss):
+        from . import doe as _doe
+        field, h, out, t4, stats = ctx.saved_tensors
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
+        ge = None
+        if g_loss is not None:
+            B, C, Ho, Wo, tB, tC = ctx.ldesc
+            ld = _lib.LossDesc(B=B, C=C, H=Ho, W=Wo, tB=tB, tC=tC)
+            ge = torch.empty((1, B, C, Ho, Wo), dtype=torch.complex64, device=out.device)
+            g = g_loss.detach().float().contiguous()
+            with torch.cuda.device(out.device):
+                _lib.check(_lib.lib().thz_intensity_mse_backward(
+                    ctypes.byref(ld), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(t4.data_ptr()),
+                    ctypes.c_void_p(stats.data_ptr()), ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(ge.data_ptr()),
+                    _stream_handle()))
+        if g_out is not None:
+            ge = g_out if ge is None else ge + g_out
+        if ge is None:
+            return (None,) * 11
+        gm = asm_apply(ge, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
+        gf = gh = None
+        pend = ctx.pend
+        if pend is None:
+            gf = gm
+        else:
+            gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
+                                            ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+        return gf, gh, None, None, None, None, None, None, None, None, None
+
+
+def asm_propagate_loss(x, target, wavelengths, spacing, z, pad_h, pad_w, unpad=True, bandlimit="exact", pend=None):
+    """Differentiable ASM to one plane fused with the QAT loss: (out [1,B,C,Ho,Wo], loss []).
+    ``pend`` (doe.PendingModulation, not yet formed): propagate its modulation of ``pend.field``
+    (``x`` is then ignored), as asm_propagate_modulated."""
+    bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
+    field, height = (pend.field, pend.height) if pend is not None else (x, None)
+    return _AsmLossFunction.apply(field, height, target, pend, list(map(float, wavelengths)),
+                                  tuple(map(float, spacing)), [float(z)], int(pad_h), int(pad_w), bool(unpad), bl)
+
+
+class _Deferral(threading.local):
+    active = False
+
+
+_DEFER = _Deferral()
+
+
+@contextlib.contextmanager
+def deferred_output():
+    """Inside this block ASM_prop.forward returns its output field unevaluated: the propagation
+    runs when the field's ``data`` is first read -- or, when the first reader is the QAT loss
+    (optics.field_intensity_mse), as one pipeline with the loss folded into its last pass
+    (thz_asm_forward_loss).  The trainers wrap their forward in it; the deferred propagation reads
+    its input field when it runs, so the input must not be modified in between."""
+    prev = _DEFER.active
+    _DEFER.active = True
+    try:
+        yield
+    finally:
+        _DEFER.active = prev
+
+
+def deferring():
+    return _DEFER.active
 
 
 def fft_rows(x, inverse=False):

@@ -24,6 +24,7 @@ import torch.distributed as dist
 import torch.nn as nn
 
 from quantizationawarethzdoe_amd import optics as _optics
+from quantizationawarethzdoe_amd import propagation as _prop
 from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
 from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
 from quantizationawarethzdoe_amd.Components.Thin_Lens import Thin_LensElement
@@ -196,8 +197,14 @@ class QATTrainer:
     # The step in two phases around the one collective; the eager step and the captured graphs
     # run the same two functions (fwd/bwd + pack | all-reduce | unpack + Adam).
     def _fb(self, frac):
-        out = self.system(frac)
-        loss = self.loss_fn(out.data, self.target)
+        if self.loss_fn is _optics.intensity_mse:
+            # the default loss folded into the last propagation
+            with _prop.deferred_output():
+                out = self.system(frac)
+            loss = _optics.field_intensity_mse(out, self.target)
+        else:
+            out = self.system(frac)
+            loss = self.loss_fn(out.data, self.target)
         loss.backward()
         self.allreduce.pack()
         return loss

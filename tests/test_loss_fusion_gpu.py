@@ -1,0 +1,157 @@
+"""Fused ASM -> QAT loss (thz_asm_forward_loss): the row-inverse pass of the last
+propagation accumulates mean((normalize(|E|^2) - target)^2) over the rows it stores.
+
+Checked against the separate path (asm_propagate -> intensity_mse, the two-kernel loss) and the
+fp64 oracle (oracle/thz_oracle.py intensity_mse of the oracle ASM, Props/ASM_Prop.py:314-378 +
+experiment_four_focal_spots.ipynb:336-370).  The output field is the same K1/K2/K3 pipeline, so
+it matches the separate path bit for bit; the loss is a one-pass fp64 sum against fp32 two-pass
+sums, rel <= 1e-5; gradients rel-L2 <= 1e-5 (same kernels, the loss statistics agree to fp32
+rounding).  Against the fp64 oracle: rel <= 1e-4 (fp32 propagation).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import thz_oracle as orc
+from tests.golden_io import rel_l2
+
+pytestmark = pytest.mark.gpu
+C0 = 2.998e8
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+# (B, C, H, W, padding_scale, target broadcast): P = 300 mixed-radix (cfg4 / cfg5), power of two,
+# runtime plan; targets broadcast over B and / or C as the notebooks' do
+CASES = [
+    ((1, 1, 100, 100), 2, (1, 1)),
+    ((3, 1, 100, 100), 2, (3, 1)),
+    ((2, 2, 100, 100), 2, (1, 2)),
+    ((1, 1, 512, 512), 2, (1, 1)),
+    ((2, 1, 256, 256), 2, (1, 1)),
+    ((2, 2, 60, 70), 2, (2, 2)),
+]
+
+
+def _wl(C):
+    return [C0 / 300e9, C0 / 250e9][:C]
+
+
+@pytest.mark.parametrize("shape,ps,tb", CASES)
+def test_asm_loss_fused_equals_separate(shape, ps, tb):
+    from quantizationawarethzdoe_amd import optics, propagation as P
+    dev = _dev()
+    B, C, H, W = shape
+    g = torch.Generator().manual_seed(3)
+    x = (torch.randn(shape, generator=g) + 1j * torch.randn(shape, generator=g)).to(torch.complex64).to(dev)
+    tgt = torch.rand((tb[0], tb[1], H, W), generator=g).to(dev)
+    wl, sp, z = _wl(C), (1e-3, 1e-3), 0.12
+    ph, pw = P.asm_padding(H, W, (ps, ps))
+    res = []
+    for fused in (True, False):
+        xd = x.clone().requires_grad_(True)
+        if fused:
+            out, loss = P.asm_propagate_loss(xd, tgt, wl, sp, z, ph, pw)
+        else:
+            out = P.asm_propagate(xd, wl, sp, [z], ph, pw)
+            loss = optics.intensity_mse(out[0], tgt)
+        loss.backward()
+        res.append((out.detach().cpu(), float(loss.detach()), xd.grad.cpu()))
+    (o1, l1, g1), (o2, l2, g2) = res
+    assert rel_l2(o1.numpy(), o2.numpy()) <= 1e-7  # same pipeline (the K3 variant only adds the sums)
+    assert abs(l1 - l2) <= 1e-5 * abs(l2)
+    assert rel_l2(g1.numpy(), g2.numpy()) <= 1e-5
+    # the fp64 oracle: propagate, then the loss
+    xo = x.cpu().to(torch.complex128)
+    oo = orc.asm_forward(xo, wl, sp, z, padding_scale=ps)
+    lo = float(orc.intensity_mse(oo, tgt.cpu().double()))
+    assert abs(l1 - lo) <= 1e-4 * abs(lo)
+
+
+def test_asm_loss_out_cotangent_adds():
+    """When the fused output field is used besides the loss, its cotangent adds to the loss's."""
+    from quantizationawarethzdoe_amd import optics, propagation as P
+    dev = _dev()
+    shape = (2, 1, 100, 100)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(shape, dtype=torch.complex64, generator=g).to(dev)
+    tgt = torch.rand((1, 1, 100, 100), generator=g).to(dev)
+    ph, pw = P.asm_padding(100, 100, (2, 2))
+    res = []
+    for fused in (True, False):
+        xd = x.clone().requires_grad_(True)
+        if fused:
+            out, loss = P.asm_propagate_loss(xd, tgt, _wl(1), (1e-3, 1e-3), 0.2, ph, pw)
+        else:
+            out = P.asm_propagate(xd, _wl(1), (1e-3, 1e-3), [0.2], ph, pw)
+            loss = optics.intensity_mse(out[0], tgt)
+        (loss + 0.3 * out.abs().pow(2).sum()).backward()
+        res.append(xd.grad.cpu())
+    assert rel_l2(res[0].numpy(), res[1].numpy()) <= 1e-5
+
+
+def test_intensity_mse_argmax_tie_and_vs_oracle():
+    """The one-pass loss kernel: a tied maximum takes the first index (torch.max), the loss and
+    the field gradient match the fp64 oracle / autograd of the reference formula."""
+    from quantizationawarethzdoe_amd import optics
+    dev = _dev()
+    g = torch.Generator().manual_seed(9)
+    f = torch.randn((3, 2, 33, 47), dtype=torch.complex64, generator=g)
+    f[1, 0, 4, 5] = 10.0
+    f[1, 1, 20, 7] = -10.0  # same |E|^2, later index: the gradient's max path stays at the first
+    t = torch.rand((1, 2, 33, 47), generator=g)
+    fd = f.to(dev).requires_grad_(True)
+    loss = optics.intensity_mse(fd, t.to(dev))
+    loss.backward()
+    fr = f.to(torch.complex128).requires_grad_(True)
+    inten = fr.abs() ** 2
+    m = inten.reshape(3, -1).max(1, keepdim=True)[0].reshape(3, 1, 1, 1)
+    lr = ((inten / m - t.double()) ** 2).mean()
+    lr.backward()
+    assert abs(float(loss) - float(lr)) <= 1e-5 * float(lr)
+    assert abs(float(loss) - float(orc.intensity_mse(f.to(torch.complex128), t.double()))) <= 1e-5 * float(lr)
+    assert rel_l2(fd.grad.cpu().numpy(), fr.grad.numpy().astype(np.complex64)) <= 1e-5
+
+
+def test_trainers_default_loss_is_fused_and_matches():
+    """QATTrainer with the default loss runs the fused pipeline; a loss_fn that is not the default
+    object runs the separate kernels.  Same seeds -> same loss trajectory and weights."""
+    from quantizationawarethzdoe_amd import optics, qat
+    dev = _dev()
+    traj = []
+    for fused in (True, False):
+        torch.manual_seed(0)
+        system = qat.FourFocalSpotsSystem(device=dev)
+        lf = None if fused else (lambda d, t: optics.intensity_mse(d, t))
+        tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=20, loss_fn=lf)
+        torch.manual_seed(11)
+        losses = [float(tr.step(f)) for f in (0.1, 0.2, 0.5, 0.9)]
+        traj.append((losses, [p.detach().cpu() for p in system.parameters() if p.requires_grad]))
+    (la, wa), (lb, wb) = traj
+    assert np.allclose(la, lb, rtol=2e-5, atol=0)
+    for a, b in zip(wa, wb):
+        assert rel_l2(a.numpy(), b.numpy()) <= 1e-4
+
+
+def test_donn_default_loss_fused_matches():
+    from quantizationawarethzdoe_amd import donn, optics
+    dev = _dev()
+    g = torch.Generator().manual_seed(2)
+    u = torch.rand(8, 1, 100, 100, generator=g).to(dev)
+    labels = torch.randint(0, 10, (8,), generator=g).to(dev)
+    out = []
+    for fused in (True, False):
+        torch.manual_seed(4)
+        model = donn.DONN(device=dev)
+        lf = None if fused else (lambda d, t: optics.intensity_mse(d, t))
+        tr = donn.DONNTrainer(model, donn.detector_targets(device=dev), loss_fn=lf)
+        torch.manual_seed(6)
+        out.append(([float(tr.step(u, labels)) for _ in range(3)], [p.detach().cpu() for p in tr.params]))
+    (la, pa), (lb, pb) = out
+    assert np.allclose(la, lb, rtol=2e-5, atol=0)
+    for a, b in zip(pa, pb):
+        assert rel_l2(a.numpy(), b.numpy()) <= 1e-4
