@@ -149,7 +149,8 @@ class DONNTrainer:
         self.chained = chained
         self.loss_fn = loss_fn
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph)
+        self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph,
+                                          fused=bool(self.params) and self.params[0].is_cuda)
         self.allreduce = GradientAllReduce(self.params, group=group)
         self.itr = 0
         self._graphs = {}

@@ -183,7 +183,10 @@ class QATTrainer:
         self.graph = graph
         # loss(out_field_data, target): the fused HIP |E|^2 -> normalize -> MSE by default
         self.loss_fn = loss_fn or _optics.intensity_mse
-        self.optimizer = torch.optim.Adam(system.parameters(), lr=lr, capturable=graph)
+        params = list(system.parameters())
+        # one fused Adam kernel per step on the GPU (torch's multi-tensor path launches ~7 small kernels)
+        self.optimizer = torch.optim.Adam(params, lr=lr, capturable=graph,
+                                          fused=bool(params) and params[0].is_cuda)
         self.allreduce = GradientAllReduce(list(system.parameters()), group=group)
         self.itr = 0
         self._graphs = {}
