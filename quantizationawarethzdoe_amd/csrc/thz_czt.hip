@@ -341,23 +341,31 @@ __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu
   czb_line(img, tw, lane, a.pa.nb, G, ld, st);
 }
 
-// pass B (columns, H axis) of V -> out [BC][outW][outH]: out[p][q] = F0 * U * z dxo dyo lambda
+// pass B (columns, H axis) of V -> out [BC][outW][outH]: out[p][q] = F0 * U * z dxo dyo lambda.
+// One workgroup per 16-column block of V (one wave per column).  A block's CZB_BS rows of the 16
+// columns are one contiguous 64 KiB run of V: the workgroup loads it coalesced (16 B per lane) and
+// transposes it through LDS, so each wave reads its column from LDS instead of one 8-byte
+// element per 128-byte line from L2.
+constexpr int CZB_TP = CZB_BS + 1;  // LDS tile row (one column): +1 element spreads the banks
+constexpr size_t czb_cols_lds_bytes() { return czb_lds_bytes(CZB_WC) + (size_t)CZB_WC * CZB_TP * sizeof(float2); }
+
 template <bool PARTIAL>
 __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_cols_blk(const float2* __restrict__ V, float2* __restrict__ out,
                                                            const float2* __restrict__ ws, CztArgs a) {
+  static_assert(CZB_WC == CB, "one workgroup per V column block");
   extern __shared__ float2 lds[];
   const wf::Tabs tw = wf::fill_tables(lds, threadIdx.x, blockDim.x);
   float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int id = blockIdx.x * CZB_WC + (threadIdx.x >> 6);
-  if (id >= a.BC * a.outH) return;
-  const int bc = id / a.outH, q = id - bc * a.outH;
+  float2* tile = reinterpret_cast<float2*>(reinterpret_cast<float*>(lds + wf::TAB) + CZB_WC * wf::IMG);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int bc = blockIdx.x / a.ncbA, qb = blockIdx.x - bc * a.ncbA;
+  const int q = qb * CZB_WC + wave;
+  const bool live = q < a.outH;  // every wave takes part in the tile loads and barriers
   const int c = bc % a.C;
   const float lam = a.lam[c];
   const float k = 6.283185307179586f / lam;
   const RsPhase rph = rs_phase(lam, a.z);
-  const float2* col = V + (size_t)bc * a.ncbA * CB * a.H + vcol(q, 0, a.H);
+  const float4* vblk = reinterpret_cast<const float4*>(V + ((size_t)bc * a.ncbA + qb) * CB * a.H);
   const float2* pre = ws + a.preB + (size_t)c * a.tabStride;
   const float2* post = ws + a.postB + (size_t)c * a.tabStride;
   const float2* G = ws + a.ftB + (size_t)c * a.pb.nb * wf::N;
@@ -366,21 +374,48 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
   const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
   const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
   const float cst = ((a.z * a.odx) * a.ody) * lam;
-  auto ld = [&](int h0, int u) {
-    float2 x = make_float2(0.f, 0.f), ph = make_float2(0.f, 0.f);
-    if (!PARTIAL || h0 + u < m) {
-      x = (col + (size_t)h0 * VHS)[(size_t)u * VHS];
-      ph = (pre + h0)[u];
+  const float2* mine = tile + wave * CZB_TP;
+  float2 acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = make_float2(0.f, 0.f);
+  for (int b = 0; b < a.pb.nb; ++b) {
+    const int h0 = CZB_BS * b;
+    // the block's [CZB_BS rows][16 columns] run: 4 x 16 B per thread, coalesced
+    float4 t4[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = (int)threadIdx.x + 1024 * i;  // float4 index: row e / 8, columns 2 (e % 8) + {0, 1}
+      t4[i] = (!PARTIAL || h0 + (e >> 3) < m) ? vblk[(size_t)h0 * (CB / 2) + e] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    return cmul(x, ph);
-  };
+    __syncthreads();  // the previous block's readers are done with the tile
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = (int)threadIdx.x + 1024 * i, row = e >> 3, col = 2 * (e & 7);
+      tile[col * CZB_TP + row] = make_float2(t4[i].x, t4[i].y);
+      tile[(col + 1) * CZB_TP + row] = make_float2(t4[i].z, t4[i].w);
+    }
+    __syncthreads();
+    if (live) {
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const float2* Gb = G + (size_t)b * wf::N + ln;
+      auto mac = [&](int i, float2 x) { acc[i] = cadd(acc[i], cmul(x, Gb[64 * (i >> 2) + 256 * (i & 3)])); };
+      auto ldb = [&](int u) {
+        if (PARTIAL && h0 + u >= m) return make_float2(0.f, 0.f);
+        return cmul(mine[u], (pre + h0)[u]);
+      };
+      wf::forward<true>(img, tw, ln, ldb, mac);
+    }
+  }
+  if (!live) return;
   auto st = [&](int, int p, float2 v) {
     if (p < M) {
       const float2 F0 = rs_kernel_fast(lin(xlo, xhi, a.outH, p), yq, a.z, k, rph);
       dst[(size_t)p * a.outH] = cscale(cmul(F0, cmul(v, post[p])), cst);
     }
   };
-  czb_line(img, tw, lane, a.pb.nb, G, ld, st);
+  auto sv = [&](int qq, int j, float2 v) { st(qq - 8, j - CZB_BS, v); };
+  wf::inverse<8>(img, tw, lane, acc, sv);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -604,7 +639,7 @@ static int czt_lds_attr() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
-    const int mx = (int)fft_lds_bytes(FFT_MAX_N);
+    const int mx = (int)std::max(fft_lds_bytes(FFT_MAX_N), czb_cols_lds_bytes());
     const void* ks[] = {
         (const void*)czt_rows_blk<false>, (const void*)czt_rows_blk<true>,
         (const void*)czt_cols_blk<false>, (const void*)czt_cols_blk<true>,
@@ -706,7 +741,7 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   {
     KernelTimer kt("czt_cols", s);
     if (a.pb.nb) {
-      hipLaunchKernelGGL(d->H % CZB_BS ? czt_cols_blk<true> : czt_cols_blk<false>, dim3((a.BC * d->outH + CZB_WC - 1) / CZB_WC), dim3(64 * CZB_WC), czb_lds_bytes(CZB_WC),
+      hipLaunchKernelGGL(d->H % CZB_BS ? czt_cols_blk<true> : czt_cols_blk<false>, dim3(a.BC * a.ncbA), dim3(64 * CZB_WC), czb_cols_lds_bytes(),
                          s, (const float2*)V, (float2*)out, (const float2*)ws, a);
     } else {
       THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
