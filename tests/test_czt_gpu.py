@@ -72,13 +72,15 @@ def test_czt_backward_vs_oracle_autograd(H, W, out, C):
     assert rel_l2(gx.cpu().numpy(), ro_g.numpy()) <= 1e-3, rel_l2(gx.cpu().numpy(), ro_g.numpy())
 
 
-@pytest.mark.parametrize("H,W,out,C", [(2048, 2048, 512, 2), (1800, 2048, 400, 1), (1300, 1100, 256, 3)])
+@pytest.mark.parametrize("H,W,out,C", [(2048, 2048, 512, 2), (1800, 2048, 400, 1), (1300, 1100, 256, 3),
+                                         (1301, 1100, 256, 1), (1302, 1024, 200, 2)])
 def test_czt_overlap_add_vs_oracle(H, W, out, C):
     """cfg3-sized CZT, forward and backward vs the fp64 oracle, rel-L2 <= 1e-3.  The forward passes
     run the overlap-add Bluestein kernels (czt_rows_blk / czt_cols_blk: 512-input blocks, 1024-point
     wave transforms): 4 full blocks per line (2048 -> 512, the cfg3 geometry), a partial last block
-    (m = 1800) and 3 blocks with M < 512 over 3 wavelengths; the backward runs the np2 adjoint
-    kernels on the same tables."""
+    (m = 1800) and 3 blocks with M < 512 over 3 wavelengths; odd H (no mirrored row pairs: each
+    wave evaluates its own RS factors) and an odd number of row pairs (the last workgroup's second
+    pair idle); the backward runs the np2 adjoint kernels on the same tables."""
     from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
     from quantizationawarethzdoe_amd.Props.CZT_Prop import CZT_prop
     rng = np.random.default_rng(H + out)
