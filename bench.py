@@ -60,7 +60,7 @@ def z_planes(rank, world):
     return [float(zs[i]) for i in shard_planes(total, rank, world)]
 
 
-def cpu_baseline(budget_s=20.0, max_planes=8):
+def cpu_baseline(budget_s=20.0, max_planes=8, progress=False):
     """The oracle (PyTorch-CPU restatement of the reference op sequence, oracle/thz_oracle.py:105-119:
     per-call transfer-function rebuild, four fftshifts, full P x P FFTs) timed on this host's cores on
     a bounded sample of the same workload: whole 4096^2 planes of the 64-plane sweep, spread over
@@ -78,6 +78,8 @@ def cpu_baseline(budget_s=20.0, max_planes=8):
     while n < max_planes:
         orc.asm_forward(x, lam, sp, zs[(n * stride) % len(zs)], 1)
         n += 1
+        if progress:
+            print(f"cpu_baseline: plane {n}/{max_planes} {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
@@ -356,9 +358,14 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=8, help="cpu_baseline sample size (whole 4096^2 planes)")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="cpu_baseline time budget, seconds")
     ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 / cfg5 secondary measurements")
+    ap.add_argument("--cpu-only", action="store_true",
+                    help="time only the cpu_baseline leg (e.g. --cpu-planes 64 --cpu-budget 1e9 for the whole sweep)")
     ap.add_argument("--dry-run", action="store_true",
                     help="rehearse the rank orchestration on the CPU (gloo, propagation stubbed, no GPU)")
     args = ap.parse_args()
+    if args.cpu_only:
+        print(json.dumps({"cpu_baseline": cpu_baseline(args.cpu_budget, args.cpu_planes, progress=True)}))
+        return
     launch_ranks(args)
     ranks = Ranks(args.dry_run)
     rank, world, dev = ranks.rank, ranks.world, ranks.dev
