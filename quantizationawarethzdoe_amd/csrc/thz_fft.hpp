@@ -346,21 +346,14 @@ __device__ __forceinline__ float2 twat(const TwLds& s, int i) { return cmul(s.t[
 // LDS slots of the twiddle tables of a length-n transform (placed after the data rows)
 __host__ __device__ constexpr int tw_lds_count(int n) { return n >= 1024 ? 64 + n / 64 + 256 : 0; }
 
-// Fill the tables (visible after the first stage's barrier).  Generated in place with
-// double-precision sincospi -- the same values as the host table, without a global load whose
-// latency every workgroup would pay before issuing its data loads.
+// Fill the tables (visible after the first stage's barrier): a gather of 64 + N/64 + 256 entries
+// of the plan's global table (tw[t] = w^t, L2-resident), issued ahead of the data loads.
 template <int N>
-__device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__, int tid, int nt) {
+__device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__ tw, int tid, int nt) {
   constexpr int N2 = 64 + N / 64;
   for (int i = tid; i < tw_lds_count(N); i += nt) {
-    double sn, cs;
-    if (i < N2) {
-      const int t = i < 64 ? i : (i - 64) * 64;
-      sincospi(-2.0 * (double)t / (double)N, &sn, &cs);
-    } else {
-      sincospi(-2.0 * (double)(i - N2) / 256.0, &sn, &cs);
-    }
-    dst[i] = make_float2((float)cs, (float)sn);
+    const int t = i < 64 ? i : (i < N2 ? (i - 64) * 64 : (i - N2) * (N / 256));
+    dst[i] = tw[t];
   }
   return TwLds{dst, dst + N2};
 }

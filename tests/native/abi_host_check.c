@@ -1,0 +1,120 @@
+/*
+ * Host-side checks of libthzdoe's C-ABI that need no GPU: descriptor validation of every entry
+ * point (null pointers, bad shapes, broadcast rules, workspace too small), the error codes and
+ * thread-local messages, and the workspace / band queries.  Built and run against the
+ * AddressSanitizer build of the library (make -C quantizationawarethzdoe_amd/csrc asan), so
+ * any host out-of-bounds access or leak on these paths aborts the run.  No kernel is launched.
+ */
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/thzdoe.h"
+
+static int fails = 0;
+#define EXPECT(cond, what)                                          \
+  do {                                                              \
+    if (!(cond)) {                                                  \
+      fprintf(stderr, "FAIL %s:%d %s (last error: %s)\n", __FILE__, \
+              __LINE__, what, thz_last_error());                    \
+      ++fails;                                                      \
+    }                                                               \
+  } while (0)
+
+int main(void) {
+  EXPECT(thz_version() && strlen(thz_version()) > 0, "version string");
+  float wl[2] = {1e-3f, 1.2e-3f}, zs[3] = {0.02f, 0.05f, 0.12f};
+
+  /* ASM: workspace and band queries on valid descriptors, rejections on bad ones */
+  thz_asm_desc a;
+  memset(&a, 0, sizeof a);
+  a.B = 1; a.C = 2; a.H = 100; a.W = 120; a.pad_h = 100; a.pad_w = 120; a.unpad = 1;
+  a.bandlimit = THZ_BANDLIMIT_EXACT; a.Z = 3; a.dx = 1e-3f; a.dy = 1e-3f; a.wavelengths = wl; a.z = zs;
+  size_t ws = 0;
+  EXPECT(thz_asm_workspace_size(&a, &ws) == THZ_OK && ws > 0, "asm workspace size");
+  int ncols = 0, zc = 0;
+  EXPECT(thz_asm_band(&a, &ncols, &zc) == THZ_OK && ncols > 0 && ncols <= 360 && zc >= 1 && zc <= 3, "asm band");
+  EXPECT(thz_asm_workspace_size(NULL, &ws) != THZ_OK, "asm null descriptor");
+  EXPECT(thz_asm_workspace_size(&a, NULL) != THZ_OK, "asm null size pointer");
+  thz_asm_desc b = a;
+  b.H = 0;
+  EXPECT(thz_asm_workspace_size(&b, &ws) != THZ_OK && strlen(thz_last_error()) > 0, "asm bad shape");
+  b = a; b.Z = 0;
+  EXPECT(thz_asm_workspace_size(&b, &ws) != THZ_OK, "asm Z = 0");
+  b = a; b.Z = THZ_MAX_Z + 1;
+  EXPECT(thz_asm_workspace_size(&b, &ws) != THZ_OK, "asm Z too large");
+  b = a; b.adjoint = 1;
+  EXPECT(thz_asm_workspace_size(&b, &ws) != THZ_OK, "asm adjoint needs Z == 1");
+  b = a; b.C = THZ_MAX_WAVELENGTHS + 1;
+  EXPECT(thz_asm_workspace_size(&b, &ws) != THZ_OK, "asm too many wavelengths");
+  EXPECT(thz_asm_forward(&a, NULL, NULL, NULL, 0, NULL) != THZ_OK, "asm forward null data");
+  char dummy[64];
+  EXPECT(thz_asm_forward(&a, dummy, dummy, dummy, 8, NULL) == THZ_E_WORKSPACE, "asm workspace too small");
+
+  /* fused entries: shape agreement is checked before anything runs */
+  thz_doe_desc m;
+  memset(&m, 0, sizeof m);
+  m.B = 1; m.C = 2; m.H = 100; m.W = 100; m.hs = 100; m.ws = 100;
+  EXPECT(thz_asm_forward_modulated(&a, &m, dummy, (const float*)dummy, NULL, NULL, dummy, dummy, 1 << 20, NULL) != THZ_OK,
+         "modulated: DOE field shape must match the ASM input");
+  thz_loss_desc l;
+  memset(&l, 0, sizeof l);
+  l.B = 1; l.C = 2; l.H = 100; l.W = 120; l.tB = 1; l.tC = 1;
+  EXPECT(thz_asm_forward_loss(&a, NULL, dummy, NULL, NULL, NULL, &l, (const float*)dummy, dummy, (float*)dummy,
+                              (float*)dummy, dummy, 1 << 20, NULL) != THZ_OK,
+         "loss: needs Z == 1");
+  b = a; b.Z = 1;
+  l.tC = 3;
+  EXPECT(thz_asm_forward_loss(&b, NULL, dummy, NULL, NULL, NULL, &l, (const float*)dummy, dummy, (float*)dummy,
+                              (float*)dummy, dummy, 1 << 20, NULL) != THZ_OK,
+         "loss: target must broadcast");
+  l.tC = 1; l.W = 99;
+  EXPECT(thz_asm_forward_loss(&b, NULL, dummy, NULL, NULL, NULL, &l, (const float*)dummy, dummy, (float*)dummy,
+                              (float*)dummy, dummy, 1 << 20, NULL) != THZ_OK,
+         "loss: shape must match the ASM output");
+  l.W = 120;
+  EXPECT(thz_intensity_mse_workspace_size(&l) >= 3 * sizeof(float), "loss workspace size");
+  EXPECT(thz_intensity_mse_workspace_size(NULL) == 0, "loss workspace null");
+  EXPECT(thz_intensity_mse_forward(&l, NULL, NULL, NULL, NULL, NULL) != THZ_OK, "loss forward null pointers");
+
+  /* CZT and RSC */
+  thz_czt_desc c;
+  memset(&c, 0, sizeof c);
+  c.B = 1; c.C = 2; c.H = 256; c.W = 256; c.outH = 64; c.outW = 64; c.dx = 5e-4f; c.dy = 5e-4f;
+  c.odx = 2.5e-4f; c.ody = 2.5e-4f; c.z = 0.5f; c.wavelengths = wl;
+  EXPECT(thz_czt_workspace_size(&c, &ws) == THZ_OK && ws > 0, "czt workspace size");
+  thz_czt_desc c2 = c;
+  c2.outW = 32;
+  EXPECT(thz_czt_workspace_size(&c2, &ws) != THZ_OK, "czt non-square output");
+  c2 = c; c2.wavelengths = NULL;
+  EXPECT(thz_czt_workspace_size(&c2, &ws) != THZ_OK, "czt null wavelengths");
+  thz_rsc_desc r;
+  memset(&r, 0, sizeof r);
+  r.B = 1; r.C = 1; r.H = 64; r.W = 64; r.dx = 1e-3f; r.dy = 1e-3f; r.z = 0.3f; r.wavelengths = wl;
+  EXPECT(thz_rsc_workspace_size(&r, &ws) == THZ_OK && ws > 0, "rsc workspace size");
+  thz_rsc_desc r2 = r;
+  r2.H = 0;
+  EXPECT(thz_rsc_workspace_size(&r2, &ws) != THZ_OK, "rsc bad shape");
+  r2 = r; r2.vectorial = 1; r2.adjoint = 1;
+  EXPECT(thz_rsc_workspace_size(&r2, &ws) != THZ_OK, "rsc vectorial adjoint");
+
+  /* elementwise entries */
+  EXPECT(thz_gaussian_beam(NULL, NULL, NULL) != THZ_OK, "gaussian null");
+  EXPECT(thz_thin_lens(NULL, NULL, NULL, NULL) != THZ_OK, "lens null");
+  EXPECT(thz_aperture(NULL, NULL, NULL, NULL) != THZ_OK, "aperture null");
+  EXPECT(thz_doe_modulate_forward(NULL, NULL, NULL, NULL, NULL, NULL, NULL) != THZ_OK, "modulate null");
+  EXPECT(thz_quant_forward(NULL, NULL, NULL, NULL, NULL, NULL) != THZ_OK, "quant null");
+  EXPECT(thz_resample_forward(NULL, NULL, NULL, NULL) != THZ_OK, "resample null");
+  EXPECT(thz_radial_forward(NULL, 0, 0, 0, NULL, NULL) != THZ_OK, "radial bad");
+  EXPECT(thz_fft_rows(NULL, NULL, 0, 1024, 0, NULL) != THZ_OK, "fft rows bad");
+  double ms = -1.0;
+  long n = -1;
+  EXPECT(thz_timing_reset() == THZ_OK && thz_timing_read("asm_cols", &ms, &n) == THZ_OK && n == 0,
+         "timing registry empty after reset");
+
+  if (fails) {
+    fprintf(stderr, "%d check(s) failed\n", fails);
+    return 1;
+  }
+  printf("abi host checks passed\n");
+  return 0;
+}
