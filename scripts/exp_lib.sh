@@ -13,7 +13,7 @@ python - gpurun_out/lib_$v$rep.log $v <<'PY'
 import json,sys
 d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{')][-1])
 s=d.get('secondary',{})
-print(sys.argv[2], d['value'], {k:v['avg_ms'] for k,v in d['kernels'].items()}, 'czt', s.get('cfg3_czt',{}).get('ms_per_call'), 'qat', {k:v['ms_per_it'] for k,v in s.get('cfg4_qat',{}).get('phases',{}).items()})
+print(sys.argv[2], d['value'], {k:v['avg_ms'] for k,v in d['kernels'].items()}, 'czt', s.get('cfg3_czt',{}).get('ms_per_call'), 'qat', {k:v['ms_per_it'] for k,v in s.get('cfg4_qat',{}).get('phases',{}).items()}, 'donn', {k:v['ms_per_step'] for k,v in s.get('cfg5_donn',{}).get('modes',{}).items()})
 PY
 done; done
 unset THZDOE_LIB
