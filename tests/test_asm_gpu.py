@@ -281,3 +281,51 @@ def test_asm_p300_mixed_radix_vs_oracle(zs, bl, H, W):
     lhs = torch.vdot(y.reshape(-1).to(torch.complex128), Ax.reshape(-1).to(torch.complex128))
     rhs = torch.vdot(AHy.reshape(-1).to(torch.complex128), r.reshape(-1).to(torch.complex128))
     assert abs(complex(lhs - rhs)) / abs(complex(lhs)) <= 1e-4
+
+
+def test_asm_max_planes_per_call():
+    """THZ_MAX_Z = 256 planes in one call (8 default z-chunks of 32, P = 1024): every 32nd plane
+    and both chunk edges vs the fp64 oracle at <= max(1e-4, 1.5 x the fp32 oracle's error)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply
+    dev = _dev()
+    rng = np.random.default_rng(31)
+    x = (rng.standard_normal((1, 1, 512, 512)) + 1j * rng.standard_normal((1, 1, 512, 512))).astype(np.complex64)
+    lam = wavelengths([300])
+    sp = spacing(0.5, 0.5)
+    zs = [float(v) for v in torch.linspace(0.01, 0.3, 256, dtype=torch.float64)]
+    lamf, spf = [float(lam[0])], [float(sp[0]), float(sp[1])]
+    out = asm_apply(torch.from_numpy(x).to(dev), lamf, spf, zs, 256, 256, True, 1).cpu().numpy()
+    assert out.shape == (256, 1, 1, 512, 512)
+    check = [0, 31, 32, 127, 128, 224, 255]
+    xt = torch.from_numpy(x)
+    with torch.no_grad():
+        r64 = orc.asm_forward_planes(xt.to(torch.complex128), lam.double(), sp.double(), [zs[k] for k in check], 1)
+        r32 = orc.asm_forward_planes(xt, lam, sp, [zs[k] for k in check], 1)
+        for k, (_, a), (_, b) in zip(check, r64, r32):
+            a = a.numpy()
+            floor = rel_l2(b.numpy(), a)
+            assert rel_l2(out[k], a) <= max(1e-4, 1.5 * floor), (k, zs[k], floor)
+
+
+def test_asm_largest_transform_p16384_properties():
+    """The largest compile-time transform (8192^2 field, padding 1 -> P = 16384; 1024-thread
+    workgroups), checked by size-independent properties (an fp64 oracle plane of 16384^2 is out
+    of reach of the CPU tests): the adjoint identity <A x, y> = <x, A^H y> to 1e-5 relative, and
+    energy never grows under the band-limited transfer function (|H| <= 1)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply
+    dev = _dev()
+    g = torch.Generator(device=dev).manual_seed(5)
+    N = 8192
+    x = torch.randn((1, 1, N, N), dtype=torch.complex64, device=dev, generator=g)
+    y = torch.randn((1, 1, 1, N, N), dtype=torch.complex64, device=dev, generator=g)
+    lam = [float(torch.tensor(C0 / 300e9, dtype=torch.float32))]
+    sp = [float(torch.tensor(0.5e-3, dtype=torch.float32))] * 2
+    ax = asm_apply(x, lam, sp, [0.3], N // 2, N // 2, True, 1)
+    ahy = asm_apply(y, lam, sp, [0.3], N // 2, N // 2, True, 1, adjoint=True)
+    lhs = torch.vdot(ax.reshape(-1).to(torch.complex128), y.reshape(-1).to(torch.complex128))
+    rhs = torch.vdot(x.reshape(-1).to(torch.complex128), ahy.reshape(-1).to(torch.complex128))
+    scale = float(torch.linalg.vector_norm(ax.abs().double())) * float(torch.linalg.vector_norm(y.abs().double()))
+    assert abs(complex(lhs - rhs)) <= 1e-5 * scale, (complex(lhs), complex(rhs), scale)
+    ex = float((x.abs().double() ** 2).sum())
+    eax = float((ax.abs().double() ** 2).sum())
+    assert 0.0 < eax <= ex * (1 + 1e-5), (eax, ex)

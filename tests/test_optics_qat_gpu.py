@@ -259,3 +259,23 @@ def test_addons_vs_golden(case):
     gx, = torch.autograd.grad(out.data, f.data, grad_outputs=torch.from_numpy(A[f"{k}__gout"]).to(_dev()))
     assert rel_l2(gx.cpu().numpy(), A[f"{k}__gx32"]) <= 1e-5
     assert out.spacing_host == [np.float32(case["ospacing"][0]), np.float32(case["ospacing"][1])]
+
+
+def test_qat_graph_train_history_is_per_step():
+    """QATTrainer.train in graph mode returns one loss per step: the replayed graph overwrites its
+    captured loss tensor in place, so the history keeps a copy of each.  The
+    history equals the per-step losses of an identically seeded trainer stepped by hand."""
+    from quantizationawarethzdoe_amd import qat
+    dev = _dev()
+    hist = []
+    for manual in (False, True):
+        torch.manual_seed(3)
+        system = qat.FourFocalSpotsSystem(device=dev)
+        tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=8, graph=True)
+        if manual:
+            hist.append(torch.tensor([float(tr.step()) for _ in range(8)]))
+        else:
+            h, _ = tr.train(8, log_every=0)
+            hist.append(h.float())
+    assert len(set(hist[0].tolist())) > 1, hist[0]  # not the last replay's value repeated
+    assert torch.allclose(hist[0], hist[1], rtol=1e-6, atol=0), (hist[0], hist[1])
