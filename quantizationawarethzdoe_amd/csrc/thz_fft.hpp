@@ -849,7 +849,7 @@ __device__ __forceinline__ void mx_stage(float2* lds, const float2 (&w1)[MW], co
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         if constexpr (FIRST) v[m][r] = ld(m, r, i + r * NB);
-        else v[m][r] = lds[padx(i + r * NB)];
+        else v[m][r] = lds[i + r * NB];
       }
       if constexpr (L > 1) {
         const float2 w = w1[m];
@@ -882,7 +882,7 @@ __device__ __forceinline__ void mx_stage(float2* lds, const float2 (&w1)[MW], co
         const int k = i % L;
         const int j = (i - k) * R + k;
 #pragma unroll
-        for (int r = 0; r < R; ++r) lds[padx(j + r * L)] = v[m][r];
+        for (int r = 0; r < R; ++r) lds[j + r * L] = v[m][r];
       }
     }
     __syncthreads();
