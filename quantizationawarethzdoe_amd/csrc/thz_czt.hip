@@ -51,6 +51,7 @@ struct CztArgs {
   // table offsets (in float2) inside the workspace, per wavelength stride; ft* holds the np2 filter
   // spectrum, or for an overlap-add pass the nb block spectra (nb x wf::N)
   size_t preA, postA, ftA, preB, postB, ftB, tabStride;
+  const float2* tw1024;  // the 1024-point plan's twiddle table (overlap-add wavefront transforms)
   float lam[THZ_MAX_WAVELENGTHS];
 };
 
@@ -305,7 +306,7 @@ template <bool PARTIAL>
 __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_rows_blk(const float2* __restrict__ in, float2* __restrict__ V,
                                                            const float2* __restrict__ ws, CztArgs a) {
   extern __shared__ float2 lds[];
-  const wf::Tabs tw = wf::fill_tables(lds, threadIdx.x, blockDim.x);
+  const wf::Tabs tw = wf::fill_tables(lds, a.tw1024, threadIdx.x, blockDim.x);
   float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
   __syncthreads();
   const int lane = threadIdx.x & 63;
@@ -354,7 +355,7 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
                                                            const float2* __restrict__ ws, CztArgs a) {
   static_assert(CZB_WC == CB, "one workgroup per V column block");
   extern __shared__ float2 lds[];
-  const wf::Tabs tw = wf::fill_tables(lds, threadIdx.x, blockDim.x);
+  const wf::Tabs tw = wf::fill_tables(lds, a.tw1024, threadIdx.x, blockDim.x);
   float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
   float2* tile = reinterpret_cast<float2*>(reinterpret_cast<float*>(lds + wf::TAB) + CZB_WC * wf::IMG);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -686,7 +687,9 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   if (!workspace || workspace_bytes < need)
     return fail(THZ_E_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
   if ((e = czt_lds_attr())) return e;
-  FftPlan plA, plB;
+  FftPlan plA, plB, pl1024;
+  if ((e = get_plan(1024, &pl1024))) return e;
+  a.tw1024 = pl1024.tw;
   if ((e = get_plan(a.pa.np2, &plA))) return e;
   if ((e = get_plan(a.pb.np2, &plB))) return e;
   hipStream_t s = (hipStream_t)stream;

@@ -43,15 +43,11 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// the workgroup's twiddle tables (all threads; barrier before use)
-__device__ __forceinline__ Tabs fill_tables(float2* tab, int tid, int nt) {
-  for (int t = tid; t < TAB; t += nt) {
-    const int n = t < 1024 ? 1024 : (t < 1280 ? 256 : 64);
-    const int e = t < 1024 ? t : (t < 1280 ? t - 1024 : t - 1280);
-    double sn, cs;
-    sincospi(-2.0 * (double)e / (double)n, &sn, &cs);
-    tab[t] = make_float2((float)cs, (float)sn);
-  }
+// the workgroup's twiddle tables (all threads; barrier before use): every entry is a root of the
+// 1024-point plan table tw1024[t] = exp(-2 pi i t / 1024) (fp64-rounded on the host), gathered
+// from L2 -- w256^e = tw1024[4 e], w64^e = tw1024[16 e]
+__device__ __forceinline__ Tabs fill_tables(float2* tab, const float2* __restrict__ tw1024, int tid, int nt) {
+  for (int t = tid; t < TAB; t += nt) tab[t] = tw1024[t < 1024 ? t : (t < 1280 ? 4 * (t - 1024) : 16 * (t - 1280))];
   return Tabs{tab, tab + 1024, tab + 1280};
 }
 
