@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu
                                                            const float2* __restrict__ ws, CztArgs a) {
   extern __shared__ float2 lds[];
   const wf::Tabs tw = wf::fill_tables(lds, a.tw1024, threadIdx.x, blockDim.x);
-  float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
+  float* img = wf::wave_image(lds, threadIdx.x >> 6);
   __syncthreads();
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * CZB_W + (threadIdx.x >> 6);
@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
   static_assert(CZB_WC == CB, "one workgroup per V column block");
   extern __shared__ float2 lds[];
   const wf::Tabs tw = wf::fill_tables(lds, a.tw1024, threadIdx.x, blockDim.x);
-  float* img = reinterpret_cast<float*>(lds + wf::TAB) + (threadIdx.x >> 6) * wf::IMG;
+  float* img = wf::wave_image(lds, threadIdx.x >> 6);
   float2* tile = reinterpret_cast<float2*>(reinterpret_cast<float*>(lds + wf::TAB) + CZB_WC * wf::IMG);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int bc = blockIdx.x / a.ncbA, qb = blockIdx.x - bc * a.ncbA;

@@ -51,17 +51,30 @@ __device__ __forceinline__ Tabs fill_tables(float2* tab, const float2* __restric
   return Tabs{tab, tab + 1024, tab + 1280};
 }
 
-// Exchange: this lane's values v[a] go to image position wpos(a); then nx[b] = image[rpos(b)].
+// This wave's float image behind the workgroup's tables.  Its offset is made opaque so the
+// compiler keeps the (large, constant) image base in the address register: every exchange access
+// is then that register plus a per-lane term and a small immediate, instead of one address add
+// per access (the base alone exceeds the 8-bit dword offsets of ds_write2 / ds_read2).
+__device__ __forceinline__ float* wave_image(float2* lds, int wave) {
+  int off = 2 * TAB + wave * IMG;
+  asm volatile("" : "+v"(off));
+  return reinterpret_cast<float*>(lds) + off;
+}
+
+// Exchange: this lane's values v[a] go to the PADDED image position wpos(a); then
+// nx[b] = image[rpos(b)] (padded too).  The callers write each padded position as a per-lane base
+// plus a compile-time term (pad() distributes over the schedule's index forms for lane < 64), so
+// every access is one address register and an immediate offset.
 template <int NA, int NB, class WPos, class RPos>
 __device__ __forceinline__ void exchange(float* img, const float2 (&v)[NA], WPos wpos, float2 (&nx)[NB], RPos rpos) {
 #pragma unroll
   for (int part = 0; part < 2; ++part) {
 #pragma unroll
-    for (int a = 0; a < NA; ++a) img[pad(wpos(a))] = part ? v[a].y : v[a].x;
+    for (int a = 0; a < NA; ++a) img[wpos(a)] = part ? v[a].y : v[a].x;
     wave_sync();
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const float x = img[pad(rpos(b))];
+      const float x = img[rpos(b)];
       if (part) nx[b].y = x;
       else nx[b].x = x;
     }
@@ -80,16 +93,20 @@ __device__ __forceinline__ void forward(float* img, const Tabs& tw, int lane, Ld
   dft16<false, HALF_IN>(v);
   float2 x1[16];
   // outputs y[16 i + q] -> stage 1 inputs x[i + 64 r]
-  exchange(img, v, [&](int q) { return 16 * lane + q; }, x1, [&](int r) { return lane + 64 * r; });
+  // pad(16 lane + q) = 16 lane + (lane >> 1) + q;  pad(lane + 64 r) = pad(lane) + 66 r
+  const int pl = pad(lane), w0 = 16 * lane + (lane >> 1);
+  exchange(img, v, [&](int q) { return w0 + q; }, x1, [&](int r) { return pl + 66 * r; });
   // stage 1: radix 16, L = 16, k = lane & 15: twiddle w256^(k r)
   const int k1 = lane & 15;
 #pragma unroll
   for (int r = 1; r < 16; ++r) x1[r] = cmul(x1[r], tw.t256[k1 * r]);
   dft16<false>(x1);
   // outputs y[(i - k) 16 + k + 16 q] -> stage 2 inputs x[i2 + 256 r], i2 = lane + 64 m
+  // pad((lane - k) 16 + k + 16 q) = (lane - k) 16 + k + 8 (lane >> 4) + 16 q + (q >> 1)
   float2 x2[16];
-  exchange(img, x1, [&](int q) { return (lane - k1) * 16 + k1 + 16 * q; }, x2,
-           [&](int b) { return lane + 64 * (b >> 2) + 256 * (b & 3); });
+  const int w1 = (lane - k1) * 16 + k1 + 8 * (lane >> 4);
+  exchange(img, x1, [&](int q) { return w1 + 16 * q + (q >> 1); }, x2,
+           [&](int b) { return pl + 66 * ((b >> 2) + 4 * (b & 3)); });
   // stage 2: radix 4, L = 256, k = i2: twiddle w1024^(k r)
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
@@ -112,17 +129,20 @@ __device__ __forceinline__ void inverse(float* img, const Tabs& tw, int lane, fl
 #pragma unroll
   for (int m = 0; m < 4; ++m) dft4<true>(in[4 * m], in[4 * m + 1], in[4 * m + 2], in[4 * m + 3]);
   // outputs y[4 i + q] -> stage 1 inputs x[lane + 64 r]
+  // pad(4 (lane + 64 m) + q) = 4 lane + (lane >> 3) + 264 m + q;  pad(lane + 64 r) = pad(lane) + 66 r
   float2 x1[16];
-  exchange(img, in, [&](int a) { return 4 * (lane + 64 * (a >> 2)) + (a & 3); }, x1,
-           [&](int r) { return lane + 64 * r; });
+  const int pl = pad(lane), w0 = 4 * lane + (lane >> 3);
+  exchange(img, in, [&](int a) { return w0 + 264 * (a >> 2) + (a & 3); }, x1, [&](int r) { return pl + 66 * r; });
   // stage 1: radix 16, L = 4, k = lane & 3: conj twiddle w64^(k r)
   const int k1 = lane & 3;
 #pragma unroll
   for (int r = 1; r < 16; ++r) x1[r] = cmulc(x1[r], tw.t64[k1 * r]);
   dft16<true>(x1);
   // outputs y[(i - k) 16 + k + 4 q] -> stage 2 inputs x[lane + 64 r]
+  // pad((lane - k) 16 + k + 4 q) = (lane - k) 16 + k + 2 (lane >> 2) + 4 q + (q >> 3)
   float2 x2[16];
-  exchange(img, x1, [&](int q) { return (lane - k1) * 16 + k1 + 4 * q; }, x2, [&](int r) { return lane + 64 * r; });
+  const int w1 = (lane - k1) * 16 + k1 + 2 * (lane >> 2);
+  exchange(img, x1, [&](int q) { return w1 + 4 * q + (q >> 3); }, x2, [&](int r) { return pl + 66 * r; });
   // stage 2: radix 16, L = 64, k = lane: conj twiddle w1024^(k r); outputs y[lane + 64 q]
 #pragma unroll
   for (int r = 1; r < 16; ++r) x2[r] = cmulc(x2[r], tw.t1024[lane * r]);
