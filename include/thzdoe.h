@@ -281,6 +281,15 @@ int thz_intensity_mse_backward(const thz_loss_desc* d, const void* field, const 
  * [B, C, Ho, Wo]; out, loss and stats are what thz_asm_forward and thz_intensity_mse_forward
  * return (stats: thz_intensity_mse_workspace_size bytes, valid for thz_intensity_mse_backward).
  */
+/*
+ * Its backward's first half in one pipeline: the ASM adjoint (d->adjoint == 1, Z == 1) of the loss
+ * gradient dL/dE = 2 E dL/dI at the forward output `field` (thz_intensity_mse_backward's formula,
+ * from the same target, stats and device grad_loss [1]), plus grad_out when non-NULL (the
+ * cotangent of the output field itself).  The row pass forms the gradient as it loads each row.
+ */
+int thz_asm_adjoint_loss(const thz_asm_desc* d, const thz_loss_desc* l, const void* field, const float* target,
+                         const float* stats, const float* grad_loss, const void* grad_out, void* grad_in,
+                         void* workspace, size_t workspace_bytes, thz_stream_t stream);
 int thz_asm_forward_loss(const thz_asm_desc* d, const thz_doe_desc* m, const void* field, const float* height,
                          const float* noise, float* height_full, const thz_loss_desc* l, const float* target,
                          void* out, float* loss, float* stats, void* workspace, size_t workspace_bytes,

@@ -183,7 +183,8 @@ class ASM_prop(nn.Module):
             else:
                 ph, pw = self.compute_padding(H, W, return_size_of_padding=True)
                 Ho, Wo = H + 2 * ph, W + 2 * pw
-            holder = torch.zeros((), dtype=torch.complex64, device=field.device).expand(B, C, Ho, Wo)
+            # shape-only placeholder (no fill kernel); the data comes from the pending propagation
+            holder = torch.empty((), dtype=torch.complex64, device=field.device).expand(B, C, Ho, Wo)
             Eout = ElectricField(data=holder, wavelengths=field.wavelengths, spacing=field.spacing,
                                  device=field.device)._adopt_host(field)
             Eout._pending = _PendingAsm(self, field, self._zh[:1])

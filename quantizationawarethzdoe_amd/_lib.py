@@ -27,7 +27,7 @@ BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 EXPORTED = [
     "thz_version", "thz_last_error",
     "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band", "thz_asm_forward_modulated",
-    "thz_asm_forward_loss",
+    "thz_asm_forward_loss", "thz_asm_adjoint_loss",
     "thz_czt_workspace_size", "thz_czt_forward",
     "thz_rsc_workspace_size", "thz_rsc_forward",
     "thz_doe_modulate_forward", "thz_doe_modulate_backward", "thz_quant_forward", "thz_quant_backward",
@@ -154,6 +154,8 @@ def _declare(lib):
     lib.thz_asm_forward_loss.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(DoeDesc), c_void_p, c_void_p,
                                          c_void_p, c_void_p, ctypes.POINTER(LossDesc), c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_void_p, c_size_t, c_void_p]
+    lib.thz_asm_adjoint_loss.argtypes = [ctypes.POINTER(AsmDesc), ctypes.POINTER(LossDesc), c_void_p, c_void_p,
+                                         c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]
     lib.thz_fft_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
     lib.thz_rsc_workspace_size.argtypes = [ctypes.POINTER(RscDesc), ctypes.POINTER(c_size_t)]
     lib.thz_rsc_forward.argtypes = [ctypes.POINTER(RscDesc), c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]

@@ -59,6 +59,15 @@ struct AsmArgs {
   // fused |E|^2 -> normalize -> MSE in K3's storer (thz_asm_forward_loss, Z == 1): ls.stats
   // non-null; K1 zeroes its accumulators
   LossSink ls;
+  // adjoint of the fused loss (thz_asm_adjoint_loss): the row pass's input is the loss gradient
+  // dL/dE at the forward output lg_field (thz_intensity_mse_backward's formula), plus the out
+  // cotangent `in` when that is given
+  const float2* lg_field;
+  const float* lg_gloss;
+  const float* lg_target;
+  const float* lg_stats;
+  int lg_tB, lg_tC;
+  float lg_two_inv_n;
   // mixed-radix K2 tables of the first z-chunk computed by tab_blocks extra K1 workgroups
   int tab_blocks;
   float lam[THZ_MAX_WAVELENGTHS];
@@ -200,7 +209,32 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
   const float xh = ez ? lin(-(float)a.Hin * a.dx / 2.0f, (float)a.Hin * a.dx / 2.0f, a.Hin, h) : 0.f;
   const int hsrc = a.mod_h ? doe_nearest_src(h, a.mod_hs, a.Hin) * a.mod_ws : 0;
   const float lam_c = a.lam[bc % a.C];
+  // loss gradient rows: field E, target T and the statistics of batch item b
+  const float2* lg_row = nullptr;
+  const float* lg_t = nullptr;
+  float lg_m = 0.f, lg_S = 0.f, lg_g = 0.f;
+  int lg_am = -1;
+  if (a.lg_field) {
+    const int b = bc / a.C, c = bc - b * a.C;
+    lg_row = a.lg_field + ((size_t)bc * a.Hin + h) * a.Win;
+    const int tb = a.lg_tB == 1 ? 0 : b, tc = a.lg_tC == 1 ? 0 : c;
+    lg_t = a.lg_target + (((size_t)tb * a.lg_tC + tc) * a.Hin + h) * a.Win;
+    lg_m = a.lg_stats[3 * b];
+    lg_S = a.lg_stats[3 * b + 2];
+    // the argmax relative to this row's first element (c H + h) W
+    lg_am = __float_as_int(a.lg_stats[3 * b + 1]) - (c * a.Hin + h) * a.Win;
+    lg_g = a.lg_gloss[0] * a.lg_two_inv_n;
+  }
   auto fetch = [&](int s) {
+    if (a.lg_field) {  // dL/dE = 2 E dL/dI, dL/dI = g (r / m - [argmax] S / m^2) (mse_backward_kernel)
+      const float2 e = lg_row[s];
+      const float I = loss_intensity(e);
+      const float r = I / lg_m - lg_t[s];
+      float dI = lg_g * r / lg_m;
+      if (s == lg_am) dI -= lg_g * lg_S / (lg_m * lg_m);
+      const float2 gl = make_float2(2.f * dI * e.x, 2.f * dI * e.y);
+      return in ? cadd(src[s], gl) : gl;
+    }
     if (a.mod_h) {  // DOELayer.modulate fused into the loader (Components/QuantizedDOE.py:92-126)
       const float hv = doe_noisy_h(a.mod_h, a.mod_u, hsrc + doe_nearest_src(s, a.mod_ws, a.Win), a.mod_tol);
       if (a.mod_hfull && bc == 0) a.mod_hfull[(size_t)h * a.Win + s] = hv;
@@ -1019,10 +1053,12 @@ extern "C" int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes) {
 namespace thz {
 static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const float* mh, const float* mu,
                             float* mhfull, const void* in, void* out, void* workspace, size_t workspace_bytes,
-                            thz_stream_t stream, const LossSink* ls = nullptr) {
+                            thz_stream_t stream, const LossSink* ls = nullptr, const thz_loss_desc* lg = nullptr,
+                            const float2* lg_field = nullptr, const float* lg_target = nullptr,
+                            const float* lg_stats = nullptr, const float* lg_gloss = nullptr) {
   int e = validate(d);
   if (e) return e;
-  if (!in || !out) return fail(THZ_E_ARG, "null data pointer");
+  if ((!in && !lg_field) || !out) return fail(THZ_E_ARG, "null data pointer");
   AsmGeom g;
   geometry(d, &g);
   const size_t need = ws_bytes(g);
@@ -1068,6 +1104,15 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
     a.mod_tand = m->tand;
   }
   if (ls) a.ls = *ls;
+  if (lg_field) {  // the adjoint pipeline starts from the loss gradient
+    a.lg_field = lg_field;
+    a.lg_gloss = lg_gloss;
+    a.lg_target = lg_target;
+    a.lg_stats = lg_stats;
+    a.lg_tB = lg->tB;
+    a.lg_tC = lg->tC;
+    a.lg_two_inv_n = (float)(2.0 / ((double)lg->B * lg->C * lg->H * lg->W));
+  }
 
   float2* T = (float2*)workspace;
   float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
@@ -1091,6 +1136,25 @@ extern "C" int thz_asm_forward_modulated(const thz_asm_desc* d, const thz_doe_de
                 d->B, d->C, d->H, d->W);
   if (m->hs < 1 || m->ws < 1) return fail(THZ_E_ARG, "bad height-map size %dx%d", m->hs, m->ws);
   return asm_forward_impl(d, m, height, noise, height_full, field, out, workspace, workspace_bytes, stream);
+}
+
+extern "C" int thz_asm_adjoint_loss(const thz_asm_desc* d, const thz_loss_desc* l, const void* field,
+                                     const float* target, const float* stats, const float* grad_loss,
+                                     const void* grad_out, void* grad_in, void* workspace, size_t workspace_bytes,
+                                     thz_stream_t stream) {
+  int e = validate(d);
+  if (e) return e;
+  if (!l || !field || !target || !stats || !grad_loss || !grad_in)
+    return fail(THZ_E_ARG, "null loss descriptor / field / target / stats / grad_loss / grad_in");
+  if (!d->adjoint || d->Z != 1) return fail(THZ_E_ARG, "the fused loss adjoint takes adjoint == 1, Z == 1");
+  const int Ho = d->unpad ? d->H : d->H + 2 * d->pad_h, Wo = d->unpad ? d->W : d->W + 2 * d->pad_w;
+  if (l->B != d->B || l->C != d->C || l->H != Ho || l->W != Wo)
+    return fail(THZ_E_ARG, "loss field %dx%dx%dx%d does not match the ASM output %dx%dx%dx%d", l->B, l->C, l->H, l->W,
+                d->B, d->C, Ho, Wo);
+  if (!(l->tB == 1 || l->tB == l->B) || !(l->tC == 1 || l->tC == l->C))
+    return fail(THZ_E_ARG, "target %dx%d does not broadcast over %dx%d", l->tB, l->tC, l->B, l->C);
+  return asm_forward_impl(d, nullptr, nullptr, nullptr, nullptr, grad_out, grad_in, workspace, workspace_bytes, stream,
+                          nullptr, l, (const float2*)field, target, stats, grad_loss);
 }
 
 extern "C" int thz_asm_forward_loss(const thz_asm_desc* d, const thz_doe_desc* m, const void* field,

@@ -152,6 +152,7 @@ class DONNTrainer:
         self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph,
                                           fused=bool(self.params) and self.params[0].is_cuda)
         self.allreduce = GradientAllReduce(self.params, group=group)
+        self._one = torch.ones((), dtype=torch.float32, device=model.device)
         self.itr = 0
         self._graphs = {}
         self._static = None
@@ -173,7 +174,8 @@ class DONNTrainer:
     # and the captured graphs run the same functions
     def _fb(self, u, target, frac):
         loss = self._loss(u, target, frac)
-        loss.backward()
+        # preallocated d loss / d loss: no fill kernel per step
+        loss.backward(gradient=self._one if loss.dtype == self._one.dtype and loss.device == self._one.device else None)
         self.allreduce.pack()
         return loss
 

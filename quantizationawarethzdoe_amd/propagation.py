@@ -197,9 +197,9 @@ def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=
 class _AsmLossFunction(torch.autograd.Function):
     """One z-plane of ASM (optionally of a pending DOE modulation) whose row-inverse pass also
     accumulates the QAT loss mean((normalize(|E|^2) - target)^2) (thz_asm_forward_loss).
-    Outputs (out [1,B,C,Ho,Wo], loss []).  Backward: the loss gradient of the stored field
-    (thz_intensity_mse_backward, plus the out cotangent when out is used elsewhere), the ASM
-    adjoint, then the modulate backward when a modulation was fused."""
+    Outputs (out [1,B,C,Ho,Wo], loss []).  Backward: the ASM adjoint of the loss gradient of the
+    stored field, formed in the adjoint's row pass (thz_asm_adjoint_loss; plus the out cotangent
+    when out is used elsewhere), then the modulate backward when a modulation was fused."""
 
     @staticmethod
     def forward(ctx, field, height, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
@@ -252,22 +252,29 @@ class _AsmLossFunction(torch.autograd.Function):
         from . import doe as _doe
         field, h, out, t4, stats = ctx.saved_tensors
         wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
-        ge = None
-        if g_loss is not None:
-            B, C, Ho, Wo, tB, tC = ctx.ldesc
-            ld = _lib.LossDesc(B=B, C=C, H=Ho, W=Wo, tB=tB, tC=tC)
-            ge = torch.empty((1, B, C, Ho, Wo), dtype=torch.complex64, device=out.device)
-            g = g_loss.detach().float().contiguous()
-            with torch.cuda.device(out.device):
-                _lib.check(_lib.lib().thz_intensity_mse_backward(
-                    ctypes.byref(ld), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(t4.data_ptr()),
-                    ctypes.c_void_p(stats.data_ptr()), ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(ge.data_ptr()),
-                    _stream_handle()))
-        if g_out is not None:
-            ge = g_out if ge is None else ge + g_out
-        if ge is None:
+        if g_loss is None and g_out is None:
             return (None,) * 11
-        gm = asm_apply(ge, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
+        if g_loss is None:
+            gm = asm_apply(g_out, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
+        else:
+            # the loss gradient is formed in the adjoint's row pass (thz_asm_adjoint_loss)
+            B, C, Ho, Wo, tB, tC = ctx.ldesc
+            H, W = field.shape[-2:]
+            ld = _lib.LossDesc(B=B, C=C, H=Ho, W=Wo, tB=tB, tC=tC)
+            d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, True)
+            L = _lib.lib()
+            nbytes = ctypes.c_size_t(0)
+            _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+            ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=out.device)
+            gm = torch.empty((B, C, H, W), dtype=torch.complex64, device=out.device)
+            g = g_loss.detach().float().contiguous()
+            go = g_out.contiguous() if g_out is not None else None
+            with torch.cuda.device(out.device):
+                _lib.check(L.thz_asm_adjoint_loss(
+                    ctypes.byref(d), ctypes.byref(ld), ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(t4.data_ptr()),
+                    ctypes.c_void_p(stats.data_ptr()), ctypes.c_void_p(g.data_ptr()),
+                    ctypes.c_void_p(go.data_ptr() if go is not None else 0), ctypes.c_void_p(gm.data_ptr()),
+                    ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()), _stream_handle()))
         gf = gh = None
         pend = ctx.pend
         if pend is None:

@@ -72,6 +72,14 @@ int main(void) {
                               (float*)dummy, dummy, 1 << 20, NULL) != THZ_OK,
          "loss: shape must match the ASM output");
   l.W = 120;
+  EXPECT(thz_asm_adjoint_loss(&b, &l, dummy, (const float*)dummy, (const float*)dummy, (const float*)dummy, NULL,
+                              dummy, dummy, 1 << 20, NULL) != THZ_OK,
+         "loss adjoint: needs adjoint == 1");
+  b.adjoint = 1;
+  EXPECT(thz_asm_adjoint_loss(&b, &l, NULL, (const float*)dummy, (const float*)dummy, (const float*)dummy, NULL,
+                              dummy, dummy, 1 << 20, NULL) != THZ_OK,
+         "loss adjoint: null field");
+  b.adjoint = 0;
   EXPECT(thz_intensity_mse_workspace_size(&l) >= 3 * sizeof(float), "loss workspace size");
   EXPECT(thz_intensity_mse_workspace_size(NULL) == 0, "loss workspace null");
   EXPECT(thz_intensity_mse_forward(&l, NULL, NULL, NULL, NULL, NULL) != THZ_OK, "loss forward null pointers");
