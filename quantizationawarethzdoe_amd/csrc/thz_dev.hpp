@@ -162,6 +162,36 @@ __device__ __forceinline__ float lin(float start, float end, int n, int i) {
 
 
 
+// Two consecutive pixels per lane (16-byte loads and stores when HW is even, so every pair is
+// aligned), one channel plane per blockIdx.y and a stride over the batch in blockIdx.z: the
+// elementwise kernels stream B C HW complex values with the per-pixel factor evaluated once per
+// (channel, pixel).  fac(p) gives the factor of pixel p (p < HW); out = in * factor.
+constexpr int EW_THREADS = 256;
+template <class Fac>
+__device__ __forceinline__ void ew_scale_pairs(const float2* __restrict__ in, float2* __restrict__ out, int B, int C,
+                                               int HW, Fac fac) {
+  const int c = blockIdx.y;
+  const int p0 = 2 * (blockIdx.x * EW_THREADS + (int)threadIdx.x);
+  if (p0 >= HW) return;
+  const bool two = p0 + 1 < HW;
+  const float2 t0 = fac(p0), t1 = two ? fac(p0 + 1) : make_float2(0.f, 0.f);
+  const bool vec = (HW & 1) == 0;
+  for (int b = blockIdx.z; b < B; b += gridDim.z) {
+    const size_t i = ((size_t)b * C + c) * HW + p0;
+    if (vec) {
+      const float4 v = *reinterpret_cast<const float4*>(in + i);
+      const float2 r0 = cmul(make_float2(v.x, v.y), t0), r1 = cmul(make_float2(v.z, v.w), t1);
+      *reinterpret_cast<float4*>(out + i) = make_float4(r0.x, r0.y, r1.x, r1.y);
+    } else {
+      out[i] = cmul(in[i], t0);
+      if (two) out[i + 1] = cmul(in[i + 1], t1);
+    }
+  }
+}
+inline dim3 ew_grid(int HW, int C, int B) {
+  return dim3((unsigned)((HW + 2 * EW_THREADS - 1) / (2 * EW_THREADS)), (unsigned)C, (unsigned)(B < 16 ? B : 16));
+}
+
 // ---------------------------------------------------------------------------------------------
 // DOE transmission (Components/QuantizedDOE.py:47-126), shared by the modulate kernels
 // (thz_doe.hip) and the ASM row pass that applies it in its loader (thz_asm.hip, the fused

@@ -46,21 +46,38 @@ __device__ __forceinline__ float2 transmission(float hv, float lam, const ModArg
 }
 
 // grid (pixel blocks, batch stride): t_c(h) once per pixel, thread and wavelength
-__global__ void doe_modulate_fwd(const float2* __restrict__ f, const float* __restrict__ h,
-                                 const float* __restrict__ u, float2* __restrict__ out, float* __restrict__ hfull,
-                                 ModArgs a) {
+// two pixels per lane (16-byte accesses for even HW), the noisy height of each evaluated once and
+// the transmission once per (channel, pixel), the batch strided over blockIdx.z
+__global__ void __launch_bounds__(EW_THREADS) doe_modulate_fwd(const float2* __restrict__ f, const float* __restrict__ h,
+                                                              const float* __restrict__ u, float2* __restrict__ out,
+                                                              float* __restrict__ hfull, ModArgs a) {
   const int HW = a.H * a.W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= HW) return;
-  const int y = p / a.W, x = p - y * a.W;
-  const int src = nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W);
-  const float hv = noisy_h(h, u, src, a);
-  if (hfull && blockIdx.y == 0) hfull[p] = hv;
+  const int p0 = 2 * (blockIdx.x * EW_THREADS + (int)threadIdx.x);
+  if (p0 >= HW) return;
+  const bool two = p0 + 1 < HW, vec = (HW & 1) == 0;
+  float hv[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int p = two || k == 0 ? p0 + k : p0;
+    const int y = p / a.W, x = p - y * a.W;
+    hv[k] = noisy_h(h, u, nearest_src(y, a.hs, a.H) * a.ws + nearest_src(x, a.ws, a.W), a);
+  }
+  if (hfull && blockIdx.z == 0) {
+    hfull[p0] = hv[0];
+    if (two) hfull[p0 + 1] = hv[1];
+  }
   for (int c = 0; c < a.C; ++c) {
-    const float2 t = transmission(hv, a.lam[c], a, nullptr);
-    for (int b = blockIdx.y; b < a.B; b += gridDim.y) {
-      const size_t i = ((size_t)b * a.C + c) * HW + p;
-      out[i] = cmul(f[i], t);
+    const float2 t0 = transmission(hv[0], a.lam[c], a, nullptr), t1 = transmission(hv[1], a.lam[c], a, nullptr);
+    for (int b = blockIdx.z; b < a.B; b += gridDim.z) {
+      const size_t i = ((size_t)b * a.C + c) * HW + p0;
+      if (vec) {
+        const float4 v = *reinterpret_cast<const float4*>(f + i);
+        const float2 r0 = cmul(make_float2(v.x, v.y), t0), r1 = cmul(make_float2(v.z, v.w), t1);
+        *reinterpret_cast<float4*>(out + i) = make_float4(r0.x, r0.y, r1.x, r1.y);
+      } else {
+        out[i] = cmul(f[i], t0);
+        if (two) out[i + 1] = cmul(f[i + 1], t1);
+      }
     }
   }
 }
@@ -398,8 +415,8 @@ extern "C" int thz_doe_modulate_forward(const thz_doe_desc* d, const void* field
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("doe_modulate_fwd", s);
   const int n = d->H * d->W;
-  hipLaunchKernelGGL(doe_modulate_fwd, dim3((n + 255) / 256, std::min(d->B, 64)), dim3(256), 0, s,
-                     (const float2*)field, height, noise, (float2*)out, height_full, a);
+  hipLaunchKernelGGL(doe_modulate_fwd, ew_grid(n, 1, d->B), dim3(EW_THREADS), 0, s, (const float2*)field, height,
+                     noise, (float2*)out, height_full, a);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;

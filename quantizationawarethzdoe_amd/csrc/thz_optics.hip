@@ -57,23 +57,18 @@ struct LensArgs {
   float coef[THZ_MAX_WAVELENGTHS];  // pi / (lambda f), fp32
 };
 
-__global__ void thin_lens_kernel(const float2* __restrict__ in, float2* __restrict__ out, LensArgs a) {
-  const int HW = a.H * a.W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= HW) return;
-  const int i = p / a.W, j = p - i * a.W;
-  const float xg = lin(a.gx0, a.gx1, a.H, i) * a.dx;
-  const float yg = lin(a.gy0, a.gy1, a.W, j) * a.dy;
-  const float r2 = xg * xg + yg * yg;
-  for (int c = 0; c < a.C; ++c) {
-    const float ang = -a.coef[c] * r2;
+__global__ void __launch_bounds__(EW_THREADS) thin_lens_kernel(const float2* __restrict__ in,
+                                                               float2* __restrict__ out, LensArgs a) {
+  const float coef = a.coef[blockIdx.y];
+  ew_scale_pairs(in, out, a.B, a.C, a.H * a.W, [&](int p) {
+    const int i = p / a.W, j = p - i * a.W;
+    const float xg = lin(a.gx0, a.gx1, a.H, i) * a.dx;
+    const float yg = lin(a.gy0, a.gy1, a.W, j) * a.dy;
+    const float r2 = xg * xg + yg * yg;
     float sn, cs;
-    sincos_rad(ang, &sn, &cs);
-    for (int b = 0; b < a.B; ++b) {
-      const size_t idx = ((size_t)b * a.C + c) * HW + p;
-      out[idx] = cmul(in[idx], make_float2(cs, sn));
-    }
-  }
+    sincos_rad(-coef * r2, &sn, &cs);
+    return make_float2(cs, sn);
+  });
 }
 
 struct ApertureArgs {
@@ -93,17 +88,13 @@ __device__ __forceinline__ bool aperture_open(const ApertureArgs& a, int i, int 
   return sqrtf(X * X + Y * Y) <= a.radius;
 }
 
-// grid (pixel blocks, planes): the mask is evaluated once per pixel and plane stride
-__global__ void aperture_kernel(const float2* __restrict__ in, float2* __restrict__ out, ApertureArgs a) {
-  const int HW = a.H * a.W;
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= HW) return;
-  const bool open = aperture_open(a, p / a.W, p % a.W);
-  for (int bc = blockIdx.y; bc < a.BC; bc += gridDim.y) {
-    const size_t idx = (size_t)bc * HW + p;
-    const float2 v = in[idx];
-    out[idx] = open ? v : make_float2(0.f * v.x, 0.f * v.y);
-  }
+// the mask as a complex factor (1 or 0), evaluated once per pixel: NaN / inf propagate as in the
+// reference's product field * mask
+__global__ void __launch_bounds__(EW_THREADS) aperture_kernel(const float2* __restrict__ in,
+                                                             float2* __restrict__ out, ApertureArgs a) {
+  ew_scale_pairs(in, out, a.BC, 1, a.H * a.W, [&](int p) {
+    return aperture_open(a, p / a.W, p % a.W) ? make_float2(1.f, 0.f) : make_float2(0.f, 0.f);
+  });
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -396,7 +387,8 @@ extern "C" int thz_thin_lens(const thz_lens_desc* d, const void* in, void* out, 
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("thin_lens", s);
   const int n = d->H * d->W;
-  hipLaunchKernelGGL(thin_lens_kernel, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)in, (float2*)out, a);
+  hipLaunchKernelGGL(thin_lens_kernel, ew_grid(n, a.C, a.B), dim3(EW_THREADS), 0, s, (const float2*)in, (float2*)out,
+                     a);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;
@@ -425,8 +417,8 @@ extern "C" int thz_aperture(const thz_aperture_desc* d, const void* in, void* ou
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("aperture", s);
   const int n = d->H * d->W;
-  hipLaunchKernelGGL(aperture_kernel, dim3((n + 255) / 256, std::min(a.BC, 64)), dim3(256), 0, s, (const float2*)in,
-                     (float2*)out, a);
+  hipLaunchKernelGGL(aperture_kernel, ew_grid(n, 1, a.BC), dim3(EW_THREADS), 0, s, (const float2*)in, (float2*)out,
+                     a);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;
