@@ -150,6 +150,10 @@ typedef struct thz_doe_desc {
   int hs, ws;                /* height-map size (upsampled to H, W if different) */
   float tolerance, epsilon, tand;
   const float* wavelengths;  /* host [C] */
+  const unsigned* rng;       /* optional DEVICE [2] = (seed, step): with noise == NULL the kernels draw
+                                the U[0,1) height noise per height pixel from a counter-based generator
+                                (hash of seed, step, rng_stream, index; forward and backward agree) */
+  unsigned rng_stream;
 } thz_doe_desc;
 
 int thz_doe_modulate_forward(const thz_doe_desc* d, const void* field, const float* height, const float* noise,
@@ -202,6 +206,9 @@ typedef struct thz_quant_desc {
   float phase_scale;  /* SGV3 2 pi / lambda_min * (sqrt(eps) - 1), fp32 */
   const float* dyn;   /* optional DEVICE [3] = (tau, s, beta) read by the kernels instead of the
                          fields above, so one captured HIP graph serves every schedule step */
+  const unsigned* rng; /* optional DEVICE [2] = (seed, step): with noise_exp == NULL the Gumbel
+                          kinds draw their Exp(1) noise in the kernel (see thz_doe_desc.rng) */
+  unsigned rng_stream;
 } thz_quant_desc;
 
 int thz_quant_forward(const thz_quant_desc* d, const float* weight, const float* noise_exp, float* height_full,

@@ -61,6 +61,13 @@ def _linear_tau(iter_frac, tau_min, tau_max):
     return tau_min + (tau_max - tau_min) * iter_frac
 
 
+class _DeviceNoise:
+    """Shape of a noise draw left to the kernel's counter-based generator (see _gumbel_noise)."""
+
+    def __init__(self, shape):
+        self.shape = shape
+
+
 def _scalar(v):
     return float(v.detach().cpu()) if torch.is_tensor(v) else float(v)
 
@@ -105,7 +112,7 @@ class DOELayer(nn.Module):
         data = input_field.data
         self._pending_mod = _doe.PendingModulation(data, h, input_field.wavelengths_host,
                                                    self._host_scalar("eps", epsilon), self._host_scalar("tand", tand),
-                                                   tolerance=tol)
+                                                   tolerance=tol, rng=self._rng_spec(0))
         out = ElectricField(data=data, wavelengths=input_field.wavelengths,
                             spacing=input_field.spacing)._adopt_host(input_field)
         out._pending = self._pending_mod
@@ -164,12 +171,24 @@ class DOELayer(nn.Module):
 
     def _quantize(self, kind, weight, mirror, clamp, expo=None, **kw):
         # _dyn: device (tau, s, beta) installed by a graph-capturing trainer (qat.QATTrainer)
+        if isinstance(expo, _DeviceNoise):  # the Exp(1) draw made in the kernel
+            return _doe.quantize(kind, weight, self._lut_values(), self._hmax, clamp=clamp, mirror=mirror, expo=None,
+                                 dyn=self.__dict__.get("_dyn"), rng=self._rng_spec(1), expo_shape=expo.shape, **kw)
         return _doe.quantize(kind, weight, self._lut_values(), self._hmax, clamp=clamp, mirror=mirror, expo=expo,
                              dyn=self.__dict__.get("_dyn"), **kw)
 
     def _gumbel_noise(self, shape, like):
-        """The Exp(1) draw F.gumbel_softmax makes (torch.empty_like(logits).exponential_())."""
+        """The Exp(1) draw F.gumbel_softmax makes (torch.empty_like(logits).exponential_()); with a
+        trainer's device generator installed (_rng), a marker: the quantizer kernel draws it."""
+        if self.__dict__.get("_rng") is not None:
+            return _DeviceNoise(tuple(shape))
         return torch.empty(shape, dtype=torch.float32, device=like.device).exponential_()
+
+    def _rng_spec(self, k):
+        """(device [seed, step], stream) of this layer's draw k (0 height noise, 1 Gumbel) or None.
+        Installed by a graph-capturing trainer with device_rng (qat.QATTrainer, donn.DONNTrainer)."""
+        r = self.__dict__.get("_rng")
+        return None if r is None else (r[0], r[1] + k)
 
     def _score_kw(self, wavelengths, tau):
         if getattr(self, "_wl_hint_src", None) is wavelengths:

@@ -82,6 +82,7 @@ class DoeDesc(ctypes.Structure):
         ("hs", ctypes.c_int), ("ws", ctypes.c_int),
         ("tolerance", ctypes.c_float), ("epsilon", ctypes.c_float), ("tand", ctypes.c_float),
         ("wavelengths", ctypes.POINTER(ctypes.c_float)),
+        ("rng", ctypes.c_void_p), ("rng_stream", ctypes.c_uint),
     ]
 
 
@@ -92,6 +93,7 @@ class QuantDesc(ctypes.Structure):
         ("hmax", ctypes.c_float), ("clamp", ctypes.c_float), ("tau", ctypes.c_float),
         ("iter_frac", ctypes.c_float), ("c_s", ctypes.c_float), ("s", ctypes.c_float),
         ("beta", ctypes.c_float), ("phase_scale", ctypes.c_float), ("dyn", ctypes.c_void_p),
+        ("rng", ctypes.c_void_p), ("rng_stream", ctypes.c_uint),
     ]
 
 

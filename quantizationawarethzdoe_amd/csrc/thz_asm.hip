@@ -56,6 +56,8 @@ struct AsmArgs {
   float* mod_hfull;     // optional: the noisy, upsampled height map [Hin][Win]
   int mod_hs, mod_ws;
   float mod_tol, mod_eps, mod_tand;
+  const unsigned* mod_rng;  // device generator state for the height noise when mod_u is null
+  unsigned mod_rng_stream;
   // fused |E|^2 -> normalize -> MSE in K3's storer (thz_asm_forward_loss, Z == 1): ls.stats
   // non-null; K1 zeroes its accumulators
   LossSink ls;
@@ -236,7 +238,8 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
       return in ? cadd(src[s], gl) : gl;
     }
     if (a.mod_h) {  // DOELayer.modulate fused into the loader (Components/QuantizedDOE.py:92-126)
-      const float hv = doe_noisy_h(a.mod_h, a.mod_u, hsrc + doe_nearest_src(s, a.mod_ws, a.Win), a.mod_tol);
+      const float hv = doe_noisy_h(a.mod_h, a.mod_u, hsrc + doe_nearest_src(s, a.mod_ws, a.Win), a.mod_tol,
+                                   a.mod_rng, a.mod_rng_stream);
       if (a.mod_hfull && bc == 0) a.mod_hfull[(size_t)h * a.Win + s] = hv;
       return cmul(src[s], doe_transmission(hv, lam_c, a.mod_eps, a.mod_tand, nullptr));
     }
@@ -1102,6 +1105,8 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
     a.mod_tol = m->tolerance;
     a.mod_eps = m->epsilon;
     a.mod_tand = m->tand;
+    a.mod_rng = m->rng;
+    a.mod_rng_stream = m->rng_stream;
   }
   if (ls) a.ls = *ls;
   if (lg_field) {  // the adjoint pipeline starts from the loss gradient

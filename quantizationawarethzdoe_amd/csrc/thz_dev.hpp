@@ -207,10 +207,34 @@ __device__ __forceinline__ int doe_nearest_src(int dst, int in, int out) {
   return min((int)floorf((float)dst * scale), in - 1);
 }
 
-// noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85); u == nullptr: no noise
-__device__ __forceinline__ float doe_noisy_h(const float* h, const float* u, int idx, float tol) {
+// Counter-based draws for graph-replayed training (the trainers' device_rng): every value is a
+// hash of (seed, step, stream, index) -- stateless, so a forward and its backward regenerate the
+// same draw, and each replay of a captured graph draws afresh from the step its host updates in
+// the device state rng = [seed, step].  splitmix64 finalisation of the packed counter.
+__device__ __forceinline__ unsigned long long rng_bits(const unsigned* rng, unsigned stream, unsigned idx) {
+  unsigned long long x = ((unsigned long long)(rng[0] ^ (stream * 0x9E3779B9u)) << 32) | rng[1];
+  x ^= (unsigned long long)idx * 0xD1B54A32D192ED03ull;
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+// U[0, 1) with 24 random bits (torch.rand's support)
+__device__ __forceinline__ float rng_u01(const unsigned* rng, unsigned stream, unsigned idx) {
+  return (float)(unsigned)(rng_bits(rng, stream, idx) >> 40) * (1.0f / 16777216.0f);
+}
+// Exp(1) = -log U with U in (0, 1] (Tensor.exponential_)
+__device__ __forceinline__ float rng_exp1(const unsigned* rng, unsigned stream, unsigned idx) {
+  return -logf((float)((unsigned)(rng_bits(rng, stream, idx) >> 40) + 1u) * (1.0f / 16777216.0f));
+}
+
+// noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85); u == nullptr: the device
+// generator when rng is set, else no noise
+__device__ __forceinline__ float doe_noisy_h(const float* h, const float* u, int idx, float tol,
+                                             const unsigned* rng = nullptr, unsigned stream = 0) {
   float v = h[idx];
   if (u) v = v + ((u[idx] - 0.5f) * 2.0f) * tol;
+  else if (rng) v = v + ((rng_u01(rng, stream, (unsigned)idx) - 0.5f) * 2.0f) * tol;
   return v;
 }
 

@@ -34,12 +34,14 @@ struct ModArgs {
   int bl;  // batch lanes per block of the backward (power of two <= 16)
   int has_noise;
   float tol, eps, tand;
+  const unsigned* rng;  // device generator state (when there is no noise array)
+  unsigned rng_stream;
   float lam[THZ_MAX_WAVELENGTHS];
 };
 
 __device__ __forceinline__ int nearest_src(int dst, int in, int out) { return doe_nearest_src(dst, in, out); }
 __device__ __forceinline__ float noisy_h(const float* h, const float* u, int idx, const ModArgs& a) {
-  return doe_noisy_h(h, a.has_noise ? u : nullptr, idx, a.tol);
+  return doe_noisy_h(h, a.has_noise ? u : nullptr, idx, a.tol, a.rng, a.rng_stream);
 }
 __device__ __forceinline__ float2 transmission(float hv, float lam, const ModArgs& a, float2* gamma) {
   return doe_transmission(hv, lam, a.eps, a.tand, gamma);
@@ -145,6 +147,8 @@ struct QArgs {
   int kind, hq, wq, mirror, L;
   float hmax, clampv, tau, iter_frac, c_s, s, beta, phase_scale;
   const float* dyn;  // device (tau, s, beta) overriding the three above (graph replay)
+  const unsigned* rng;  // device generator state: the Exp(1) noise drawn here when expo == nullptr
+  unsigned rng_stream;
   float lut[THZ_MAX_LUT];
   float plut_w[THZ_MAX_LUT];  // wrapped phase LUT (SGV3)
 };
@@ -247,7 +251,9 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
   float out;
   float y[THZ_MAX_LUT];
   if (a.kind == THZ_Q_NGS) {
-    const int arg = gumbel_soft(w + (size_t)p * a.L, expo + (size_t)p * a.L, a.L, q.tau, y);
+    float ex[THZ_MAX_LUT];
+    THZ_FOR_LEVELS(l, a.L) ex[l] = expo ? expo[(size_t)p * a.L + l] : rng_exp1(a.rng, a.rng_stream, (unsigned)(p * a.L + l));
+    const int arg = gumbel_soft(w + (size_t)p * a.L, ex, a.L, q.tau, y);
     out = st_value(a, y, arg);
     THZ_FOR_LEVELS(l, a.L) ysave[(size_t)p * a.L + l] = y[l];
   } else if (a.kind == THZ_Q_SGV1) {
@@ -256,7 +262,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
     THZ_FOR_LEVELS(l, a.L) {
       float dsc;
       sgv3_score(a, q.s, w[p], l, &logits[l], &dsc);
-      ex[l] = expo[(size_t)l * n + p];
+      ex[l] = expo ? expo[(size_t)l * n + p] : rng_exp1(a.rng, a.rng_stream, (unsigned)(l * n + p));
     }
     const int arg = gumbel_soft(logits, ex, a.L, q.tau, y);
     out = st_value(a, y, arg);
@@ -288,7 +294,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
       THZ_FOR_LEVELS(l, a.L) {
         float dsc;
         sgv3_score(a, q.s, phase, l, &logits[l], &dsc);
-        ex[l] = expo[(size_t)l * n + p];
+        ex[l] = expo ? expo[(size_t)l * n + p] : rng_exp1(a.rng, a.rng_stream, (unsigned)(l * n + p));
       }
       const int arg = gumbel_soft(logits, ex, a.L, q.tau, y);
       const float qv = st_value(a, y, arg);
@@ -386,6 +392,8 @@ static int qargs(const thz_quant_desc* d, QArgs* a) {
   a->beta = d->beta;
   a->phase_scale = d->phase_scale;
   a->dyn = d->dyn;
+  a->rng = d->rng;
+  a->rng_stream = d->rng_stream;
   for (int l = 0; l < d->L; ++l) {
     a->lut[l] = d->lut[l];
     // (phase_lut + pi) % 2pi - pi of the reference's LUT phases (:802), host fp32
@@ -411,6 +419,8 @@ extern "C" int thz_doe_modulate_forward(const thz_doe_desc* d, const void* field
   a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W; a.hs = d->hs; a.ws = d->ws;
   a.has_noise = noise != nullptr;
   a.tol = d->tolerance; a.eps = d->epsilon; a.tand = d->tand;
+  a.rng = d->rng;
+  a.rng_stream = d->rng_stream;
   for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("doe_modulate_fwd", s);
@@ -431,6 +441,8 @@ extern "C" int thz_doe_modulate_backward(const thz_doe_desc* d, const void* grad
   a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W; a.hs = d->hs; a.ws = d->ws;
   a.has_noise = noise != nullptr;
   a.tol = d->tolerance; a.eps = d->epsilon; a.tand = d->tand;
+  a.rng = d->rng;
+  a.rng_stream = d->rng_stream;
   for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("doe_modulate_bwd", s);
@@ -454,8 +466,8 @@ extern "C" int thz_quant_forward(const thz_quant_desc* d, const float* weight, c
   if (e) return e;
   const bool gumbel =
       d->kind == THZ_Q_NGS || d->kind == THZ_Q_SGV1 || (d->kind == THZ_Q_SGV3 && d->iter_frac > 0.3f);
-  if (!weight || !height_full || (gumbel && (!noise_exp || !y_soft)))
-    return fail(THZ_E_ARG, "null argument (Gumbel kinds need noise_exp and y_soft)");
+  if (!weight || !height_full || (gumbel && ((!noise_exp && !d->rng) || !y_soft)))
+    return fail(THZ_E_ARG, "null argument (Gumbel kinds need noise_exp or rng, and y_soft)");
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("quant_fwd", s);
   const int n = d->hq * d->wq;

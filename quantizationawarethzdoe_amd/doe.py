@@ -20,10 +20,13 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
-def _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths):
+def _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths, rng=None):
+    """``rng``: None, or (device int32 [2] = (seed, step), stream) -- the height noise is then drawn
+    in the kernels (thz_doe_desc.rng) instead of read from a noise array."""
     wl = _lib.float_array(wavelengths)
     d = _lib.DoeDesc(B=B, C=C, H=H, W=W, hs=hs, ws=ws, tolerance=float(tol), epsilon=float(eps), tand=float(tand),
-                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)))
+                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
+                     rng=rng[0].data_ptr() if rng is not None else None, rng_stream=rng[1] if rng is not None else 0)
     d._keep = wl
     return d
 
@@ -32,36 +35,38 @@ class _Modulate(torch.autograd.Function):
     """field * t(h + noise), nearest-upsampled (Components/QuantizedDOE.py:92-126)."""
 
     @staticmethod
-    def forward(ctx, field, height, noise, tol, eps, tand, wavelengths):
+    def forward(ctx, field, height, noise, tol, eps, tand, wavelengths, rng=None):
         _require_device(field, "DOE modulate")
         field = field.contiguous()
         height = height.detach().contiguous().float()
         B, C, H, W = field.shape
         hs, ws = height.shape
-        d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths)
+        d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths, rng if noise is None else None)
         out = torch.empty_like(field)
         hfull = torch.empty((H, W), dtype=torch.float32, device=field.device)
         with torch.cuda.device(field.device):
             _lib.check(_lib.lib().thz_doe_modulate_forward(ctypes.byref(d), _ptr(field), _ptr(height), _ptr(noise),
                                                            _ptr(out), _ptr(hfull), _stream_handle()))
         ctx.save_for_backward(field, height, noise)
-        ctx.cfg = (tol, eps, tand, wavelengths)
+        ctx.cfg = (tol, eps, tand, wavelengths, rng)
         ctx.mark_non_differentiable(hfull)
         return out, hfull
 
     @staticmethod
     def backward(ctx, g, _gh):
         field, height, noise = ctx.saved_tensors
-        tol, eps, tand, wavelengths = ctx.cfg
+        tol, eps, tand, wavelengths, rng = ctx.cfg
         return modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, ctx.needs_input_grad[0],
-                                 ctx.needs_input_grad[1]) + (None, None, None, None, None)
+                                 ctx.needs_input_grad[1], rng=rng) + (None, None, None, None, None, None)
 
 
-def modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, need_field=True, need_height=True):
-    """(grad_field, grad_height) of field * t(h + noise) for the output gradient g (one kernel)."""
+def modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, need_field=True, need_height=True,
+                      rng=None):
+    """(grad_field, grad_height) of field * t(h + noise) for the output gradient g (one kernel);
+    ``rng`` regenerates a device-drawn noise (see _doe_desc)."""
     B, C, H, W = field.shape
     hs, ws = height.shape
-    d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths)
+    d = _doe_desc(B, C, H, W, hs, ws, tol, eps, tand, wavelengths, rng if noise is None else None)
     g = g.contiguous()
     gf = torch.empty_like(field) if need_field else None
     gh = torch.empty((hs, ws), dtype=torch.float32, device=field.device) if need_height else None
@@ -71,20 +76,22 @@ def modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, need
     return gf, gh
 
 
-def _modulate_args(field, height, tolerance, noise):
+def _modulate_args(field, height, tolerance, noise, rng=None):
     from quantizationawarethzdoe_amd.propagation import kernel_dtype
     field = kernel_dtype(field, "DOE modulate")
-    if tolerance is not None and noise is None:
+    if tolerance is not None and noise is None and rng is None:
         noise = torch.rand_like(height)
     if noise is not None:
         noise = noise.detach().contiguous().float()
     return field, noise, 0.0 if tolerance is None else float(tolerance)
 
 
-def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None):
-    """Differentiable DOE modulation on the HIP kernel; returns (out, noisy full-size height)."""
-    field, noise, tol = _modulate_args(field, height, tolerance, noise)
-    return _Modulate.apply(field, height, noise, tol, float(eps), float(tand), tuple(map(float, wavelengths)))
+def modulate(field, height, wavelengths, eps, tand, tolerance=None, noise=None, rng=None):
+    """Differentiable DOE modulation on the HIP kernel; returns (out, noisy full-size height).
+    ``rng`` (see _doe_desc): draw the height noise on the device instead of torch.rand_like."""
+    field, noise, tol = _modulate_args(field, height, tolerance, noise, rng)
+    return _Modulate.apply(field, height, noise, tol, float(eps), float(tand), tuple(map(float, wavelengths)),
+                           rng if tolerance is not None else None)
 
 
 class PendingModulation:
@@ -95,8 +102,9 @@ class PendingModulation:
     field's data.  ``hfull`` is the noisy upsampled height map, set by whichever runs first."""
     kind = "modulation"
 
-    def __init__(self, field, height, wavelengths, eps, tand, tolerance=None, noise=None):
-        self.field, self.noise, self.tol = _modulate_args(field, height, tolerance, noise)
+    def __init__(self, field, height, wavelengths, eps, tand, tolerance=None, noise=None, rng=None):
+        self.field, self.noise, self.tol = _modulate_args(field, height, tolerance, noise, rng)
+        self.rng = rng if tolerance is not None and self.noise is None else None
         self.height = height
         self.wavelengths = tuple(map(float, wavelengths))
         self.eps, self.tand = float(eps), float(tand)
@@ -106,7 +114,7 @@ class PendingModulation:
     def run(self):
         if self.out is None:
             self.out, hf = _Modulate.apply(self.field, self.height, self.noise, self.tol, self.eps, self.tand,
-                                           self.wavelengths)
+                                           self.wavelengths, self.rng)
             if self.hfull is None:
                 self.hfull = hf
         return self.out
@@ -115,29 +123,35 @@ class PendingModulation:
         """The thz_doe_desc of this modulation (+ the arrays it points to kept alive)."""
         B, C, H, W = self.field.shape
         hs, ws = self.height.shape[-2:]
-        return _doe_desc(B, C, H, W, hs, ws, self.tol, self.eps, self.tand, self.wavelengths)
+        return _doe_desc(B, C, H, W, hs, ws, self.tol, self.eps, self.tand, self.wavelengths, self.rng)
 
 
 def _quant_desc(kind, hq, wq, mirror, lut, hmax, clamp, tau=1.0, iter_frac=0.0, c_s=0.0, s=0.0, beta=0.0,
-                phase_scale=0.0, dyn=None):
+                phase_scale=0.0, dyn=None, rng=None):
     arr = _lib.float_array(lut)
     d = _lib.QuantDesc(kind=kind, hq=hq, wq=wq, mirror=int(bool(mirror)), L=len(lut),
                        lut=ctypes.cast(arr, ctypes.POINTER(ctypes.c_float)), hmax=float(hmax), clamp=float(clamp),
                        tau=float(tau), iter_frac=float(iter_frac), c_s=float(c_s), s=float(s), beta=float(beta),
-                       phase_scale=float(phase_scale), dyn=dyn.data_ptr() if dyn is not None else None)
+                       phase_scale=float(phase_scale), dyn=dyn.data_ptr() if dyn is not None else None,
+                       rng=rng[0].data_ptr() if rng is not None else None, rng_stream=rng[1] if rng is not None else 0)
     d._keep = arr
     return d
 
 
 class _Quantize(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, weight, expo, cfg):
+    def forward(ctx, weight, expo, cfg, expo_shape=None):
         kind, hq, wq, mirror, lut, kw = cfg
         d = _quant_desc(kind, hq, wq, mirror, lut, **kw)
         w = weight.detach().contiguous().float()
         Hf, Wf = (2 * hq, 2 * wq) if mirror else (hq, wq)
         out = torch.empty((Hf, Wf), dtype=torch.float32, device=w.device)
-        ysoft = torch.empty_like(expo) if expo is not None else None
+        if expo is not None:
+            ysoft = torch.empty_like(expo)
+        elif expo_shape is not None:  # the Exp(1) noise drawn in the kernel (rng)
+            ysoft = torch.empty(expo_shape, dtype=torch.float32, device=w.device)
+        else:
+            ysoft = None
         with torch.cuda.device(w.device):
             _lib.check(_lib.lib().thz_quant_forward(ctypes.byref(d), _ptr(w), _ptr(expo), _ptr(out), _ptr(ysoft),
                                                     _stream_handle()))
@@ -154,10 +168,10 @@ class _Quantize(torch.autograd.Function):
         with torch.cuda.device(w.device):
             _lib.check(_lib.lib().thz_quant_backward(ctypes.byref(d), _ptr(w), _ptr(ysoft), _ptr(g.contiguous()),
                                                      _ptr(gw), _stream_handle()))
-        return gw, None, None
+        return gw, None, None, None
 
 
-def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, dyn=None, **kw):
+def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, dyn=None, rng=None, expo_shape=None, **kw):
     """Quantized height map of one of the QAT layers (HIP forward + backward); weight shape kept.
 
     ``dyn``: optional device float32 [3] = (tau, s, beta) the kernels read instead of the
@@ -175,9 +189,10 @@ def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, dyn=No
     if dyn is not None and (dyn.dtype != torch.float32 or not dyn.is_cuda or dyn.numel() != 3):
         raise ValueError("dyn must be a float32 device tensor of 3 values (tau, s, beta)")
     cfg = (kind, int(hq), int(wq), bool(mirror), tuple(float(v) for v in lut),
-           dict(hmax=float(hmax), clamp=float(clamp), dyn=dyn, **{k: float(v) for k, v in kw.items()}))
+           dict(hmax=float(hmax), clamp=float(clamp), dyn=dyn, rng=rng if expo is None else None,
+                **{k: float(v) for k, v in kw.items()}))
     e = expo.contiguous().float() if expo is not None else None
-    return _Quantize.apply(weight.reshape(shape), e, cfg)
+    return _Quantize.apply(weight.reshape(shape), e, cfg, tuple(expo_shape) if expo is None and expo_shape else None)
 
 
 class _Radial(torch.autograd.Function):

@@ -140,7 +140,8 @@ class DONNTrainer:
     the batch and its targets are copied into static device buffers before each replay.
     """
 
-    def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True, loss_fn=None):
+    def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True, loss_fn=None,
+                 device_rng=True):
         from quantizationawarethzdoe_amd.qat import GradientAllReduce
         self.model = model
         self.targets = targets.to(model.device).float().contiguous()
@@ -157,9 +158,15 @@ class DONNTrainer:
         self._graphs = {}
         self._static = None
         if graph:
-            self.dyn = torch.zeros(3, dtype=torch.float32, device=model.device)
-            for d in model.does:
+            # (tau, s, beta) bits + the device generator (seed, step): qat.QATTrainer's scheme; each
+            # layer draws on its own streams
+            self._state = torch.zeros(5, dtype=torch.int32, device=model.device)
+            self.dyn = self._state[:3].view(torch.float32)
+            self._seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
+            for i, d in enumerate(model.does):
                 d._dyn = self.dyn
+                if device_rng:
+                    d._rng = (self._state[3:], 2 * i)
 
     def _loss(self, u, target, frac):
         if self.loss_fn is None or self.loss_fn is _optics.intensity_mse:
@@ -238,7 +245,8 @@ class DONNTrainer:
         st.copy_(target)
         lead = self.model.does[0]
         phase = lead._graph_phase(frac)
-        self.dyn.copy_(torch.tensor(list(lead._dyn_values(frac)), dtype=torch.float32))
+        from quantizationawarethzdoe_amd.qat import _state_values
+        self._state.copy_(_state_values(lead._dyn_values(frac), self._seed, self.itr))
         if phase not in self._graphs:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]

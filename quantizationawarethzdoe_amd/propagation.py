@@ -182,7 +182,7 @@ class _AsmModulatedFunction(torch.autograd.Function):
             gk = asm_apply(g[k:k + 1], wavelengths, spacing, [z], pad_h, pad_w, unpad, bandlimit, True)
             gm = gk if gm is None else gm + gk
         gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
-                                        ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+                                        ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
         return gf, gh, None, None, None, None, None, None, None, None
 
 
@@ -281,7 +281,7 @@ class _AsmLossFunction(torch.autograd.Function):
             gf = gm
         else:
             gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
-                                            ctx.needs_input_grad[0], ctx.needs_input_grad[1])
+                                            ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
         return gf, gh, None, None, None, None, None, None, None, None, None
 
 

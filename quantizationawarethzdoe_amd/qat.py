@@ -104,6 +104,13 @@ class FourFocalSpotsSystem(nn.Module):
         return self.asm_prop3(self.doe(self.input_field, iter_frac))
 
 
+def _state_values(dyn, seed, step):
+    """Host int32 [5]: the float32 bits of (tau, s, beta), then (seed, step) of the device generator."""
+    import numpy as np
+    bits = np.asarray(dyn, dtype=np.float32).view(np.int32).tolist()
+    return torch.tensor(bits + [int(seed), int(step) & 0x7FFFFFFF], dtype=torch.int32)
+
+
 class GradientAllReduce:
     """Average the gradients of ``params`` over the process group with ONE flat all-reduce.
 
@@ -176,7 +183,8 @@ class QATTrainer:
     stream differs from the eager path (same distribution, different draws).
     """
 
-    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False, loss_fn=None):
+    def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False, loss_fn=None,
+                 device_rng=True):
         self.system = system
         self.target = target.to(system.device).float().contiguous()
         self.max_itrs = max_itrs
@@ -192,8 +200,15 @@ class QATTrainer:
         self.itr = 0
         self._graphs = {}
         if graph:
-            self.dyn = torch.zeros(3, dtype=torch.float32, device=system.device)
+            # one device state per step: (tau, s, beta) as float bits, then the generator (seed, step);
+            # with device_rng the layer's Gumbel and height-noise draws are made in the kernels from
+            # it (no torch RNG kernels, nor their per-replay offset fills, in the captured graph)
+            self._state = torch.zeros(5, dtype=torch.int32, device=system.device)
+            self.dyn = self._state[:3].view(torch.float32)
             system.doe._dyn = self.dyn
+            self._seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
+            if device_rng:
+                system.doe._rng = (self._state[3:], 0)
 
     def _frac(self, iter_frac):
         return self.itr / self.max_itrs if iter_frac is None else iter_frac
@@ -265,8 +280,7 @@ class QATTrainer:
 
     def _graph_step(self, frac):
         phase = self.system.doe._graph_phase(frac)
-        tau, sv, beta = self.system.doe._dyn_values(frac)
-        self.dyn.copy_(torch.tensor([tau, sv, beta], dtype=torch.float32))
+        self._state.copy_(_state_values(self.system.doe._dyn_values(frac), self._seed, self.itr))
         if phase not in self._graphs:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]

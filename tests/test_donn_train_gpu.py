@@ -90,7 +90,7 @@ def test_donn_trainer_graph_matches_eager_with_fixed_noise():
         orig = torch.rand_like
         torch.rand_like = lambda t, *a, **k: unif.clone()
         try:
-            tr = donn.DONNTrainer(model, donn.detector_targets(device=_dev()), graph=graph)
+            tr = donn.DONNTrainer(model, donn.detector_targets(device=_dev()), graph=graph, device_rng=False)
             losses[graph] = [float(tr.step(u, labels).detach()) for _ in range(6)]
         finally:
             torch.rand_like = orig

@@ -225,7 +225,7 @@ def test_qat_graph_replay_matches_eager_with_fixed_noise():
         orig = torch.rand_like
         torch.rand_like = lambda t, *a, **k: unif.clone()
         try:
-            tr = qat.QATTrainer(system, target, max_itrs=20, graph=graph)
+            tr = qat.QATTrainer(system, target, max_itrs=20, graph=graph, device_rng=False)
             losses[graph] = [float(tr.step().detach()) for _ in range(20)]
         finally:
             torch.rand_like = orig
