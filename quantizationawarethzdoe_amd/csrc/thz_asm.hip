@@ -840,11 +840,11 @@ static void geometry(const thz_asm_desc* d, AsmGeom* g) {
   g->ncbu = (g->ncols + CBU - 1) / CBU;
   int zc = d->z_chunk > 0 ? d->z_chunk : 0;
   if (zc == 0) {
-    // default: up to 32 z-planes per column pass (the forward column FFT and the T read are
-    // shared by the chunk), U capped at 5 GiB of the 288 GB HBM.  Measured on cfg2 (current
-    // kernels, 64 planes): z_chunk 16/32/64 -> 5925/6069/6113 planes/s.
+    // default: up to 64 z-planes per column pass (the forward column FFT and the T read are
+    // shared by the chunk; one K2 and one K3 launch per 64 planes), U capped at 10 GiB of the
+    // 288 GB HBM.  Measured on cfg2 (64 planes, round 2): z_chunk 32 / 64 -> 6830 / 7270 planes/s.
     const double per_z = (double)g->BC * g->ncbu * CBU * g->Hout * sizeof(float2);
-    zc = (int)std::max(1.0, std::min(32.0, std::floor((5120.0 * 1024 * 1024) / per_z)));
+    zc = (int)std::max(1.0, std::min(64.0, std::floor((10240.0 * 1024 * 1024) / per_z)));
   }
   g->zc = std::min(zc, d->adjoint ? 1 : d->Z);
 }

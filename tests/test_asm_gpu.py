@@ -163,7 +163,7 @@ def _cfg2_input(dev):
 
 
 def test_asm_cfg2_timed_path_vs_oracle():
-    """The exact kernels the headline bench times: asm_cols<8192> with a 32-plane z-chunk (spectrum
+    """The headline kernels over several z-chunks: asm_cols<8192> with a 32-plane z-chunk (spectrum
     reused across z in registers, per-z kept-row bisection), the kfull / kparts z-range split of
     the last dispatch round, and a tail chunk of 8 planes.  40 planes over 20-120 mm (the bench
     sweep's range, experiment_extend_depth_of_focus.ipynb:229); the first and last plane of each
@@ -195,6 +195,28 @@ def test_asm_cfg2_timed_path_vs_oracle():
         assert rel_l2(g[::64, ::64], G[f"p{p}__sub64"]) <= 1e-4
         assert rel_l2(g[2048], G[f"p{p}__row64"]) <= 1e-4
         assert abs(float(np.sum(np.abs(g) ** 2)) - float(G[f"p{p}__energy64"])) <= 1e-5 * float(G[f"p{p}__energy64"])
+
+
+def test_asm_cfg2_default_chunk_vs_oracle():
+    """The bench's own launch: 64 planes of the cfg2 sweep at the library's default z_chunk (one
+    64-plane column pass and one row pass); planes 0, 31, 32 and 63 vs the fp32 oracle (<= 1e-4)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_plan_info
+    dev = _dev()
+    x, lam = _cfg2_input(dev)
+    sp = [float(torch.tensor(0.25e-3, dtype=torch.float32))] * 2
+    zs = [float(v) for v in torch.linspace(20e-3, 120e-3, 64, dtype=torch.float64)]
+    ncols, zc = asm_plan_info(1, 1, 4096, 4096, 2048, 2048, True, 1, [lam], sp, zs)
+    assert zc == 64
+    out = asm_apply(x, [lam], sp, zs, 2048, 2048, True, 1)
+    check = [0, 31, 32, 63]
+    got = {k: out[k, 0, 0].cpu().numpy() for k in check}
+    del out
+    with torch.no_grad():
+        refs = orc.asm_forward_planes(x.cpu(), torch.tensor([lam], dtype=torch.float32), torch.tensor(sp),
+                                      [zs[k] for k in check], 1)
+        for k, (_, ref) in zip(check, refs):
+            e = rel_l2(got[k], ref[0, 0].numpy())
+            assert e <= 1e-4, (k, zs[k], e)
 
 
 def test_asm_p2048_64_planes_every_plane_vs_oracle():
