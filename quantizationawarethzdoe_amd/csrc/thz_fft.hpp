@@ -338,7 +338,10 @@ __device__ __noinline__ void stage_generic(float2* lds, int n, int L, int R, con
 // wait behind the kernel's outstanding global stores).
 struct TwLds {
   const float2* t;     // t[a] = w^a (a < 64), t[64 + b] = w^(64 b), w = exp(-2 pi i / N)
-  const float2* t256;  // exp(-2 pi i m / 256), m < 256: every twiddle of the L R = 256 stage
+  // every twiddle of the L R = 256 stage as a 16 x 16 table, t256[16 r + k] = exp(-2 pi i r k / 256):
+  // the 16 butterflies k of a half-wave read 16 consecutive slots for each r (conflict-free; the
+  // flat table t[r k] put 2 to 4 distinct slots on one bank for r = 4, 8, 12)
+  const float2* t256;
 };
 __device__ __forceinline__ float2 twat(const float2* __restrict__ p, int i) { return p[i]; }
 __device__ __forceinline__ float2 twat(const TwLds& s, int i) { return cmul(s.t[i & 63], s.t[64 + (i >> 6)]); }
@@ -352,7 +355,8 @@ template <int N>
 __device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restrict__ tw, int tid, int nt) {
   constexpr int N2 = 64 + N / 64;
   for (int i = tid; i < tw_lds_count(N); i += nt) {
-    const int t = i < 64 ? i : (i < N2 ? (i - 64) * 64 : (i - N2) * (N / 256));
+    const int q = i - N2;
+    const int t = i < 64 ? i : (i < N2 ? (i - 64) * 64 : (q >> 4) * (q & 15) * (N / 256));
     dst[i] = tw[t];
   }
   return TwLds{dst, dst + N2};
@@ -395,6 +399,21 @@ __host__ __device__ constexpr int c64_c(int L) { return L == 1 ? 1 : (L < 16 ? L
 template <int L>
 __host__ __device__ constexpr int c64_lay(int j) { return j + c64_c(L) * (j >> c64_sh(L)); }
 
+// Butterfly order of a stage that reads the natural-order (padx) image: each 32-lane half reads
+// x[i + r NB] for 32 butterflies, which under padx land on float2 slots i + (i >> 4): 32
+// consecutive i put slot 0 and slot 32 of the run on one bank (2-way on every read).  Swapping
+// bits 4 and 8 of the thread index gives each half the runs [16b, 16b + 16) and
+// [16b + 256, 16b + 272), whose padded slots 17b + l and 17b + 272 + l cover the 64 banks once
+// (17 * 16 = 272 = 16 mod 32).  Any butterfly order is valid for a stage whose results go back
+// to LDS; the twiddle index i mod L is unchanged (L <= 16 in these stages).
+template <int LIN, int T, int NB, bool OUT_LDS>
+__device__ __forceinline__ int stage_order(int tid) {
+  if constexpr (LIN == 1 && OUT_LDS && T % 512 == 0 && NB % 512 == 0)
+    return (tid & ~0x110) | ((tid & 0x10) << 4) | ((tid & 0x100) >> 4);
+  else
+    return tid;
+}
+
 template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, int LIN = 1, int LOUT = L, class Tw,
           class Ld, class Sv>
 __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
@@ -403,10 +422,11 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
   static_assert(MB * T == NB, "pow2 plan must tile exactly");
   static_assert(NB % 16 == 0, "constant-offset LDS addressing");
   constexpr int TWS = N / (L * R);
+  const int bo = IN_LDS ? stage_order<LIN, T, NB, OUT_LDS>(tid) : tid;
   float2 v[MB][R];
 #pragma unroll
   for (int m = 0; m < MB; ++m) {
-    const int i = tid + m * T;
+    const int i = bo + m * T;
     if constexpr (IN_LDS) {
       const float2* src = lds + c64_lay<LIN>(i);
 #pragma unroll
@@ -418,10 +438,11 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     if constexpr (L > 1) {
       float2 w[R];
       if constexpr (L * R == 256 && std::is_same<Tw, TwLds>::value) {
-        // w^r = exp(-2 pi i k r / 256) with k r <= 225: straight LDS reads, no products
+        // w^r = exp(-2 pi i k r / 256): straight LDS reads of the 16 x 16 table, no products
+        static_assert(L == 16, "the L R = 256 stage of a radix-16 schedule");
         const int k = i & (L - 1);
 #pragma unroll
-        for (int r = 1; r < R; ++r) w[r] = tw.t256[k * r];
+        for (int r = 1; r < R; ++r) w[r] = tw.t256[16 * r + k];
       } else {
         twiddle_powers<R>(tw, (i & (L - 1)) * TWS, w);
       }
@@ -434,7 +455,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
-      const int i = tid + m * T;
+      const int i = bo + m * T;
       const int k = i & (L - 1);
       const int i0 = m * T, k0 = i0 & (L - 1), j0 = (i0 - k0) * R + k0;  // thread 0: folds after unrolling
       float2* dst = lds + c64_lay<LOUT>((i - k) * R + k);
@@ -445,7 +466,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
   } else {
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
-      const int i = tid + m * T;
+      const int i = bo + m * T;
       const int k = L * R == N ? i : i & (L - 1);  // last stage: i < N / R = L
       const int j = (i - k) * R + k;
 #pragma unroll
@@ -679,9 +700,10 @@ __device__ __forceinline__ void stage_core(const Tw& tw, int tid, In& in, float2
     if constexpr (L > 1) {
       float2 w[R];
       if constexpr (L * R == 256 && std::is_same<Tw, TwLds>::value) {
+        static_assert(L == 16, "the L R = 256 stage of a radix-16 schedule");
         const int k = i & (L - 1);
 #pragma unroll
-        for (int r = 1; r < R; ++r) w[r] = tw.t256[k * r];
+        for (int r = 1; r < R; ++r) w[r] = tw.t256[16 * r + k];
       } else {
         twiddle_powers<R>(tw, (i & (L - 1)) * TWS, w);
       }

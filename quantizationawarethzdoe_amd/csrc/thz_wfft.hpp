@@ -47,7 +47,12 @@ __device__ __forceinline__ void wave_sync() {
 // 1024-point plan table tw1024[t] = exp(-2 pi i t / 1024) (fp64-rounded on the host), gathered
 // from L2 -- w256^e = tw1024[4 e], w64^e = tw1024[16 e]
 __device__ __forceinline__ Tabs fill_tables(float2* tab, const float2* __restrict__ tw1024, int tid, int nt) {
-  for (int t = tid; t < TAB; t += nt) tab[t] = tw1024[t < 1024 ? t : (t < 1280 ? 4 * (t - 1024) : 16 * (t - 1280))];
+  // t256 as a 16 x 16 table [r][k] = w256^(r k): stage 1's 16 butterflies k read 16 consecutive
+  // slots per r (the flat w256^(k r) put 2 to 4 distinct slots on one bank for r = 4, 8, 12)
+  for (int t = tid; t < TAB; t += nt) {
+    const int q = t - 1024;
+    tab[t] = tw1024[t < 1024 ? t : (t < 1280 ? 4 * (q >> 4) * (q & 15) : 16 * (t - 1280))];
+  }
   return Tabs{tab, tab + 1024, tab + 1280};
 }
 
@@ -99,7 +104,7 @@ __device__ __forceinline__ void forward(float* img, const Tabs& tw, int lane, Ld
   // stage 1: radix 16, L = 16, k = lane & 15: twiddle w256^(k r)
   const int k1 = lane & 15;
 #pragma unroll
-  for (int r = 1; r < 16; ++r) x1[r] = cmul(x1[r], tw.t256[k1 * r]);
+  for (int r = 1; r < 16; ++r) x1[r] = cmul(x1[r], tw.t256[16 * r + k1]);
   dft16<false>(x1);
   // outputs y[(i - k) 16 + k + 16 q] -> stage 2 inputs x[i2 + 256 r], i2 = lane + 64 m
   // pad((lane - k) 16 + k + 16 q) = (lane - k) 16 + k + 8 (lane >> 4) + 16 q + (q >> 1)
