@@ -29,7 +29,14 @@
 #include "thz_common.hpp"
 #include "thz_dev.hpp"
 
+
 namespace thz {
+
+// non-temporal (streaming) 8-byte store
+__device__ __forceinline__ void st_stream(float2* p, float2 v) {
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(f32x2{v.x, v.y}, reinterpret_cast<f32x2*>(p));
+}
 
 constexpr float TWO_PI_F = 6.283185307179586f;  // (float)(2*pi), as torch casts the python scalar
 
@@ -410,6 +417,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
+        // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2;
+        // streaming stores here ran K2 4.1 -> 13.8 ms)
         if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v;
       };
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
@@ -610,7 +619,14 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     ibase = (unsigned)((lc * a.Hout + r) * a.Wout);
   }
   auto put = [&](int w, float2 v) {
-    dst[w] = v;
+    if constexpr (PN >= 1024 && !is_mx(PN)) {
+      // large planes: written once and not read back by this pipeline, so streaming (non-temporal)
+      // stores that do not displace the U lines the neighbouring rows' workgroups still gather
+      // (cfg2: K3 4.71 -> 4.45 ms).  The small P = 300 layers' outputs feed the next layer from L2.
+      st_stream(dst + w, v);
+    } else {
+      dst[w] = v;
+    }
     if constexpr (LOSS) acc.add(v, trow[w], ibase + (unsigned)w);
   };
   if constexpr (is_mx(PN)) {
