@@ -33,6 +33,7 @@
 #include "thz_dev.hpp"
 #include "thz_wfft.hpp"
 
+
 namespace thz {
 
 struct BluePass {
@@ -331,7 +332,11 @@ __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu
     const float2 F = rs_kernel_fast(xh, lin(ylo, yhi, a.W, w), a.z, k, rph);
     float2 x = make_float2(0.f, 0.f), pw = make_float2(0.f, 0.f);
     if (!PARTIAL || w < m) {
-      x = (src + w0)[u];
+      {  // the input rows are read once: streaming loads keep the L2 for the block spectra and tables
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 t = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(src + w0) + u);
+        x = make_float2(t.x, t.y);
+      }
       pw = (pre + w0)[u];
     }
     return cmul(cmul(x, F), pw);
@@ -386,7 +391,13 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = (int)threadIdx.x + 1024 * i;  // float4 index: row e / 8, columns 2 (e % 8) + {0, 1}
-      t4[i] = (!PARTIAL || h0 + (e >> 3) < m) ? vblk[(size_t)h0 * (CB / 2) + e] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!PARTIAL || h0 + (e >> 3) < m) {
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+        const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(vblk) + (size_t)h0 * (CB / 2) + e);
+        t4[i] = make_float4(t.x, t.y, t.z, t.w);
+      } else {
+        t4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
     __syncthreads();  // the previous block's readers are done with the tile
 #pragma unroll
