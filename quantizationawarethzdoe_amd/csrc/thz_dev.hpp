@@ -176,9 +176,19 @@ __device__ __forceinline__ void ew_scale_pairs(const float2* __restrict__ in, fl
   const bool two = p0 + 1 < HW;
   const float2 t0 = fac(p0), t1 = two ? fac(p0 + 1) : make_float2(0.f, 0.f);
   const bool vec = (HW & 1) == 0;
+  // fields of 64 MB and more stream through the caches (read once, written once, and larger
+  // than the L2s); smaller ones (the P = 300 layers' fields) stay cache-resident for their consumer
+  const bool stream = (size_t)B * C * HW >= ((size_t)8 << 20);
   for (int b = blockIdx.z; b < B; b += gridDim.z) {
     const size_t i = ((size_t)b * C + c) * HW + p0;
     if (vec) {
+      typedef float f32x4 __attribute__((ext_vector_type(4)));
+      if (stream) {
+        const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(in + i));
+        const float2 r0 = cmul(make_float2(v.x, v.y), t0), r1 = cmul(make_float2(v.z, v.w), t1);
+        __builtin_nontemporal_store(f32x4{r0.x, r0.y, r1.x, r1.y}, reinterpret_cast<f32x4*>(out + i));
+        continue;
+      }
       const float4 v = *reinterpret_cast<const float4*>(in + i);
       const float2 r0 = cmul(make_float2(v.x, v.y), t0), r1 = cmul(make_float2(v.z, v.w), t1);
       *reinterpret_cast<float4*>(out + i) = make_float4(r0.x, r0.y, r1.x, r1.y);
