@@ -49,9 +49,18 @@ extern "C" {
 
 typedef void* thz_stream_t; /* hipStream_t */
 
+/* ABI of this header.  Bumped whenever a descriptor struct changes layout (round 2 appended
+ * rng / rng_stream to thz_doe_desc and thz_quant_desc): a caller compares thz_abi_version()
+ * with the THZ_ABI_VERSION it was compiled against before its first call, since a shorter
+ * struct from an older header would make the library read past it.  Descriptors are plain C
+ * structs: zero-initialise them (memset / `= {0}` / ctypes defaults) so fields a caller does not
+ * know about stay 0 (no noise buffer and no device generator means no noise). */
+#define THZ_ABI_VERSION 3
+
 /* Library identity. */
 const char* thz_version(void);
 const char* thz_last_error(void);
+int thz_abi_version(void);
 
 /*
  * Angular-spectrum propagation, Props/ASM_Prop.py:314-378 (forward) and its

@@ -175,7 +175,15 @@ class ASM_prop(nn.Module):
     def forward(self, field: ElectricField) -> ElectricField:
         """pad -> ft2 -> x H -> ift2 -> crop (Props/ASM_Prop.py:314-378), on the MI355X kernels.
         Inside propagation.deferred_output() the returned field carries the propagation unevaluated
-        (_PendingAsm) so the QAT loss can be folded into it."""
+        (_PendingAsm) so the QAT loss can be folded into it.
+
+        One z per call, as the reference: its transfer function exp(i z sqrt(k^2 - K^2)) broadcasts
+        a multi-valued z against [1, C, P, P] (:253) and does not give one plane per z.  A z with
+        several values raises ValueError naming propagate_planes (all planes in one call) instead of
+        propagating only its first value."""
+        if len(self._zh) != 1:
+            raise ValueError(f"ASM_prop.forward propagates one z-plane; z has {len(self._zh)} values -- use "
+                             f"propagate_planes(field, z_list) for [Z, B, C, H, W] in one call")
         if _prop.deferring():
             B, C, H, W = field.shape
             if not (self.do_padding and not self.do_unpad_after_pad):
@@ -187,9 +195,9 @@ class ASM_prop(nn.Module):
             holder = torch.empty((), dtype=torch.complex64, device=field.device).expand(B, C, Ho, Wo)
             Eout = ElectricField(data=holder, wavelengths=field.wavelengths, spacing=field.spacing,
                                  device=field.device)._adopt_host(field)
-            Eout._pending = _PendingAsm(self, field, self._zh[:1])
+            Eout._pending = _PendingAsm(self, field, self._zh)
             return Eout
-        out = self._run(field, self._zh[:1])
+        out = self._run(field, self._zh)
         Eout = ElectricField(data=out[0], wavelengths=field.wavelengths, spacing=field.spacing, device=field.device)
         return Eout._adopt_host(field)
 

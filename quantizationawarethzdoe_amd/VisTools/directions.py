@@ -20,18 +20,23 @@ def get_random_weights(weights, generator=None):
 
 
 def normalize_direction(direction, weights):
-    """d *= |w| / (|d| + 1e-10) per tensor (:102-104)."""
+    """d_i *= |w_i| / (|d_i| + 1e-10) for each pair (:102-104).  The reference calls it with one
+    parameter's direction and weight tensors (:111), so the pairs are their slices along dim 0:
+    every filter (row) of d is scaled to the norm of the matching row of w (Li et al.'s
+    filter-wise normalisation)."""
     for d, w in zip(direction, weights):
         d.mul_(w.norm() / (d.norm() + 1e-10))
 
 
 def normalize_directions_for_weights(direction, weights):
-    """(:106-111): 0- and 1-d parameters get a zero direction, the rest the filter-wise norm."""
+    """(:106-111): 0- and 1-d parameters get a zero direction, the rest are normalised filter by
+    filter (slices along dim 0) as the reference's ``normalize_direction(d, w)`` does."""
     assert len(direction) == len(weights)
     for d, w in zip(direction, weights):
         if d.dim() <= 1:
             d.fill_(0)
-        normalize_direction([d], [w])
+            continue
+        normalize_direction(d, w)
 
 
 def create_random_direction(model, generator=None):

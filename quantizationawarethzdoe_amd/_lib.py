@@ -20,12 +20,13 @@ THZ_E_WORKSPACE = 3
 THZ_E_HIP = 4
 THZ_MAX_WAVELENGTHS = 64
 THZ_MAX_Z = 256
+THZ_ABI_VERSION = 3  # include/thzdoe.h: the descriptor layouts below
 
 BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 
 # every symbol include/thzdoe.h declares (checked by tests/test_abi.py)
 EXPORTED = [
-    "thz_version", "thz_last_error",
+    "thz_version", "thz_last_error", "thz_abi_version",
     "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band", "thz_asm_forward_modulated",
     "thz_asm_forward_loss", "thz_asm_adjoint_loss",
     "thz_czt_workspace_size", "thz_czt_forward",
@@ -200,6 +201,10 @@ def lib():
                                        "(make -C quantizationawarethzdoe_amd/csrc)")
                 h = ctypes.CDLL(LIB_PATH)
                 _declare(h)
+                abi = h.thz_abi_version()
+                if abi != THZ_ABI_VERSION:
+                    raise ThzError(-1, f"{LIB_PATH} has ABI {abi}, these bindings describe ABI {THZ_ABI_VERSION}: "
+                                       "rebuild the library (make -C quantizationawarethzdoe_amd/csrc)")
                 _lib = h
     return _lib
 

@@ -160,13 +160,10 @@ class DONNTrainer:
         if graph:
             # (tau, s, beta) bits + the device generator (seed, step): qat.QATTrainer's scheme; each
             # layer draws on its own streams
-            self._state = torch.zeros(5, dtype=torch.int32, device=model.device)
-            self.dyn = self._state[:3].view(torch.float32)
-            self._seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
-            for i, d in enumerate(model.does):
-                d._dyn = self.dyn
-                if device_rng:
-                    d._rng = (self._state[3:], 2 * i)
+            from quantizationawarethzdoe_amd.qat import StepState
+            seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
+            self._step_state = StepState(model.device, seed, device_rng)
+            self.dyn = self._step_state.dyn
 
     def _loss(self, u, target, frac):
         if self.loss_fn is None or self.loss_fn is _optics.intensity_mse:
@@ -213,27 +210,28 @@ class DONNTrainer:
                for p in self.params if p in self.optimizer.state}
         side = torch.cuda.Stream(device=self.model.device)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(2):  # allocator, autograd and Adam's lazy state, outside the capture
-                self.optimizer.zero_grad(set_to_none=True)
-                self._fb(su, st, frac)
+        with self._step_state.installed(self.model.does):
+            with torch.cuda.stream(side):
+                for _ in range(2):  # allocator, autograd and Adam's lazy state, outside the capture
+                    self.optimizer.zero_grad(set_to_none=True)
+                    self._fb(su, st, frac)
+                    self._opt()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            with torch.no_grad():  # the warm-up must not move the training trajectory
+                for p, v in zip(self.params, p0):
+                    p.copy_(v)
+                for p in self.params:
+                    saved = st0.get(id(p))
+                    for k, v in self.optimizer.state.get(p, {}).items():
+                        if torch.is_tensor(v):
+                            v.copy_(saved[k]) if saved is not None else v.zero_()
+            self.optimizer.zero_grad(set_to_none=True)
+            g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_fb):
+                loss = self._fb(su, st, frac)
+            with torch.cuda.graph(g_opt):
                 self._opt()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        with torch.no_grad():  # the warm-up must not move the training trajectory
-            for p, v in zip(self.params, p0):
-                p.copy_(v)
-            for p in self.params:
-                saved = st0.get(id(p))
-                for k, v in self.optimizer.state.get(p, {}).items():
-                    if torch.is_tensor(v):
-                        v.copy_(saved[k]) if saved is not None else v.zero_()
-        self.optimizer.zero_grad(set_to_none=True)
-        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
-            loss = self._fb(su, st, frac)
-        with torch.cuda.graph(g_opt):
-            self._opt()
         return g_fb, g_opt, loss
 
     def _graph_step(self, u, target, frac):
@@ -245,8 +243,7 @@ class DONNTrainer:
         st.copy_(target)
         lead = self.model.does[0]
         phase = lead._graph_phase(frac)
-        from quantizationawarethzdoe_amd.qat import _state_values
-        self._state.copy_(_state_values(lead._dyn_values(frac), self._seed, self.itr))
+        self._step_state.upload(lead._dyn_values(frac), self.itr)
         if phase not in self._graphs:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]

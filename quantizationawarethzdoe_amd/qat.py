@@ -17,6 +17,7 @@ MI355X mapping
 """
 from __future__ import annotations
 
+import contextlib
 import time
 
 import torch
@@ -104,11 +105,58 @@ class FourFocalSpotsSystem(nn.Module):
         return self.asm_prop3(self.doe(self.input_field, iter_frac))
 
 
-def _state_values(dyn, seed, step):
-    """Host int32 [5]: the float32 bits of (tau, s, beta), then (seed, step) of the device generator."""
-    import numpy as np
-    bits = np.asarray(dyn, dtype=np.float32).view(np.int32).tolist()
-    return torch.tensor(bits + [int(seed), int(step) & 0x7FFFFFFF], dtype=torch.int32)
+class StepState:
+    """The per-step device state of a graph-replayed trainer: int32 [5] = the float32 bits of the
+    layer schedule (tau, s, beta), then the device generator's (seed, step).
+
+    ``upload`` writes the host values into one slot of a pinned ring and enqueues an asynchronous
+    copy into the device state on the current stream: no pageable (synchronous) host->device copy
+    per step.  A slot is rewritten only after the copy that last read it has run (one event per
+    slot), so the host may run up to ``depth`` steps ahead of the GPU.
+
+    ``installed(layers)`` puts the state on the layers (``_dyn``; with device_rng also ``_rng``,
+    two draw streams per layer) for the duration of a capture only: the captured kernels keep the
+    pointers, while eager forwards after training draw from torch's generator and use their own
+    iter_frac, as the reference's layers do."""
+
+    def __init__(self, device, seed, device_rng, depth=8):
+        import numpy as np
+        self.state = torch.zeros(5, dtype=torch.int32, device=device)
+        self.dyn = self.state[:3].view(torch.float32)
+        self.seed = seed
+        self.device_rng = device_rng
+        self._pinned = torch.zeros(depth, 5, dtype=torch.int32).pin_memory()
+        self._host = self._pinned.numpy()
+        self._np = np
+        self._events = [None] * depth
+        self._k = 0
+
+    def upload(self, dyn, step):
+        k = self._k
+        self._k = (k + 1) % len(self._events)
+        ev = self._events[k]
+        if ev is None:
+            ev = self._events[k] = torch.cuda.Event()
+        else:
+            ev.synchronize()
+        self._host[k, :3] = self._np.asarray(dyn, dtype=self._np.float32).view(self._np.int32)
+        self._host[k, 3] = int(self.seed)
+        self._host[k, 4] = int(step) & 0x7FFFFFFF
+        self.state.copy_(self._pinned[k], non_blocking=True)
+        ev.record()
+
+    @contextlib.contextmanager
+    def installed(self, layers):
+        for i, d in enumerate(layers):
+            d._dyn = self.dyn
+            if self.device_rng:
+                d._rng = (self.state[3:], 2 * i)
+        try:
+            yield
+        finally:
+            for d in layers:
+                d.__dict__.pop("_dyn", None)
+                d.__dict__.pop("_rng", None)
 
 
 class GradientAllReduce:
@@ -203,12 +251,9 @@ class QATTrainer:
             # one device state per step: (tau, s, beta) as float bits, then the generator (seed, step);
             # with device_rng the layer's Gumbel and height-noise draws are made in the kernels from
             # it (no torch RNG kernels, nor their per-replay offset fills, in the captured graph)
-            self._state = torch.zeros(5, dtype=torch.int32, device=system.device)
-            self.dyn = self._state[:3].view(torch.float32)
-            system.doe._dyn = self.dyn
-            self._seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
-            if device_rng:
-                system.doe._rng = (self._state[3:], 0)
+            seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
+            self._step_state = StepState(system.device, seed, device_rng)
+            self.dyn = self._step_state.dyn
 
     def _frac(self, iter_frac):
         return self.itr / self.max_itrs if iter_frac is None else iter_frac
@@ -255,32 +300,33 @@ class QATTrainer:
                for p in params if p in self.optimizer.state}
         side = torch.cuda.Stream(device=self.system.device)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                self.optimizer.zero_grad(set_to_none=True)
-                self._fb(frac)
+        with self._step_state.installed([self.system.doe]):
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    self.optimizer.zero_grad(set_to_none=True)
+                    self._fb(frac)
+                    self._opt()
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            with torch.no_grad():
+                for p, v in zip(params, p0):
+                    p.copy_(v)
+                for p in params:
+                    saved = st0.get(id(p))
+                    for k, v in self.optimizer.state[p].items():
+                        if torch.is_tensor(v):
+                            v.copy_(saved[k]) if saved is not None else v.zero_()
+            self.optimizer.zero_grad(set_to_none=True)
+            g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_fb):
+                loss = self._fb(frac)
+            with torch.cuda.graph(g_opt):
                 self._opt()
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        with torch.no_grad():
-            for p, v in zip(params, p0):
-                p.copy_(v)
-            for p in params:
-                saved = st0.get(id(p))
-                for k, v in self.optimizer.state[p].items():
-                    if torch.is_tensor(v):
-                        v.copy_(saved[k]) if saved is not None else v.zero_()
-        self.optimizer.zero_grad(set_to_none=True)
-        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fb):
-            loss = self._fb(frac)
-        with torch.cuda.graph(g_opt):
-            self._opt()
         return g_fb, g_opt, loss
 
     def _graph_step(self, frac):
         phase = self.system.doe._graph_phase(frac)
-        self._state.copy_(_state_values(self.system.doe._dyn_values(frac), self._seed, self.itr))
+        self._step_state.upload(self.system.doe._dyn_values(frac), self.itr)
         if phase not in self._graphs:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]

@@ -22,6 +22,7 @@ static int fails = 0;
 
 int main(void) {
   EXPECT(thz_version() && strlen(thz_version()) > 0, "version string");
+  EXPECT(thz_abi_version() == THZ_ABI_VERSION, "ABI version matches the header");
   float wl[2] = {1e-3f, 1.2e-3f}, zs[3] = {0.02f, 0.05f, 0.12f};
 
   /* ASM: workspace and band queries on valid descriptors, rejections on bad ones */

@@ -132,3 +132,22 @@ def test_vczt_alias_propagates_each_component(case):
     ref = np.concatenate([y, 2 * y, -1j * y], 0)
     assert out.shape == ref.shape
     assert rel_l2(out, ref) <= 1e-3
+
+
+def test_czt_cfg3_geometry_vs_reference_signature():
+    """cfg3 at its own geometry (2048^2 -> 512^2, dx 0.5 -> 0.25 mm, z = 0.5 m, 32 wavelengths over
+    220-330 GHz, all in one call as bench.py times it) vs the REFERENCE's own fp64 output signature
+    on the same seeded white inputs (tests/golden/cfg3_check.npz, tests/golden/gen_cfg3_check.py):
+    every plane's sub-grid, row 256 and energy within bench.CZT_CHECK_TOL (the reference's own fp32
+    output is up to 1.8e-2 off its fp64 here; this build's chirps are double precision)."""
+    import bench
+    from quantizationawarethzdoe_amd.propagation import czt_apply
+    freqs = torch.linspace(220e9, 330e9, 32, dtype=torch.float64)
+    lam = [float(torch.tensor(C0 / float(f), dtype=torch.float32)) for f in freqs]
+    idx = list(range(32))
+    x = torch.stack([bench.cfg3_input(i) for i in idx])[None].to("cuda:0")
+    sp = [float(torch.tensor(0.5e-3, dtype=torch.float32))] * 2
+    out = czt_apply(x, lam, sp, 0.5, 512, 512, 0.25e-3, 0.25e-3)
+    assert out.shape == (1, 32, 512, 512)
+    chk = bench.check_czt(out, idx)
+    assert chk["ok"], chk

@@ -90,8 +90,30 @@ def test_qat_graph_device_rng_deterministic_and_trains():
         torch.manual_seed(21)
         system = qat.FourFocalSpotsSystem(device=dev)
         tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=60, graph=True)
-        assert system.doe.__dict__.get("_rng") is not None
+        assert tr._step_state.device_rng
         runs.append([float(tr.step(f)) for f in np.linspace(0.0, 0.95, 60)])
     a, b = np.array(runs[0]), np.array(runs[1])
     assert np.array_equal(a, b)  # same seed -> same device draws -> same trajectory
     assert np.isfinite(a).all() and a[-10:].mean() < a[:10].mean()
+
+
+def test_eager_forward_after_graph_training_draws_fresh_noise():
+    """The trainer's device generator and schedule buffer sit on the layer only while it captures
+    (ADVICE round 2): after graph training, eager forwards draw their tolerance / Gumbel noise
+    from torch's generator again -- two calls give different noisy height maps -- and follow the
+    iter_frac they are given."""
+    from quantizationawarethzdoe_amd import qat
+    dev = _dev()
+    torch.manual_seed(5)
+    system = qat.FourFocalSpotsSystem(device=dev)
+    tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=20, graph=True)
+    for f in (0.1, 0.5, 0.9):
+        tr.step(f)
+    assert "_rng" not in system.doe.__dict__ and "_dyn" not in system.doe.__dict__
+    with torch.no_grad():
+        system(0.9)
+        h1 = system.doe.height_map.detach().clone()
+        o1 = system(0.9).data.detach().clone()
+        o2 = system(0.9).data.detach().clone()
+    assert not torch.equal(o1, o2)  # fresh tolerance noise per eager call
+    assert torch.isfinite(h1).all()

@@ -180,7 +180,12 @@ def test_doe_layer_vs_golden(case):
 # larger shapes and edge cases vs the oracle (torch CPU, autograd for the gradients)
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("hs,ws,H,W,B,C", [(37, 53, 100, 100, 2, 3), (100, 100, 100, 100, 4, 1),
-                                           (1, 1, 7, 5, 1, 2), (512, 512, 1024, 1024, 1, 2)])
+                                           (1, 1, 7, 5, 1, 2), (512, 512, 1024, 1024, 1, 2),
+                                           # the backward's batch-lane count comes from B
+                                           # (csrc/thz_doe.hip thz_doe_modulate_backward: bl = 8 at
+                                           # B = 8, bl = 16 at cfg5's per-rank 32 and the odd 37)
+                                           (100, 100, 100, 100, 8, 1), (100, 100, 100, 100, 32, 1),
+                                           (50, 50, 100, 100, 37, 2)])
 def test_modulate_vs_oracle(hs, ws, H, W, B, C):
     from quantizationawarethzdoe_amd import doe
     g = torch.Generator().manual_seed(hs * 1000 + H)

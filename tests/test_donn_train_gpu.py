@@ -44,13 +44,16 @@ def _oracle_loss(ws, u, target, noises, chained):
     return orc.intensity_mse(out, target)
 
 
+@pytest.mark.parametrize("B", [4, 32, 256], ids=["b4", "b32_cfg5_rank", "b256_cfg5_global"])
 @pytest.mark.parametrize("chained", [True, False], ids=["chained", "notebook"])
-def test_donn_step_loss_and_grads_vs_oracle(chained):
+def test_donn_step_loss_and_grads_vs_oracle(chained, B):
+    """B = 32 is cfg5's per-rank batch at 8 GPUs and B = 256 its global batch (the bench's N = 1
+    step): both run the modulate backward with 16 batch lanes and its fixed-order LDS reduction
+    (csrc/thz_doe.hip), B = 4 runs 4."""
     from quantizationawarethzdoe_amd import donn
-    g = torch.Generator().manual_seed(5)
-    B = 4
+    g = torch.Generator().manual_seed(5 + B)
     u = torch.rand(B, 1, 100, 100, generator=g)
-    labels = torch.tensor([3, 0, 7, 9])
+    labels = torch.tensor([3, 0, 7, 9]) if B == 4 else torch.randint(0, 10, (B,), generator=g)
     noises = [torch.rand(100, 100, generator=g) for _ in range(3)]
     torch.manual_seed(2)
     model = donn.DONN(device=_dev())
@@ -98,3 +101,15 @@ def test_donn_trainer_graph_matches_eager_with_fixed_noise():
     np.testing.assert_allclose(losses[True], losses[False], rtol=1e-4)
     assert rel_l2(weights[True], weights[False]) <= 1e-4
     assert losses[False][-1] < losses[False][0]
+
+
+@pytest.mark.parametrize("chained", [True, False], ids=["chained", "notebook"])
+def test_donn_step_b256_vs_reference_step(chained):
+    """The cfg5 bench step at its global batch (256) vs the REFERENCE's own fp64 step
+    (tests/golden/cfg5_check.npz, tests/golden/gen_cfg5_check.py: the reference's ElectricField,
+    ASM_prop, ApertureElement, FullPrecisionDOELayer and normalize, the same weights, batch and
+    noise): loss within 1e-4 relative, weight gradients within 1e-3 rel-L2.  bench.py runs this
+    check after timing each mode."""
+    import bench
+    chk = bench.check_donn(_dev(), chained)
+    assert chk["ok"], chk

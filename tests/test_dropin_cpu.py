@@ -13,6 +13,31 @@ from tests.golden_io import GOLDEN, manifest
 M = manifest()
 
 
+def _load_npy_dict_restricted(path):
+    """The dict .save() wrote (an object .npy holding a pickled dict), read with an unpickler that
+    resolves only numpy's array / dtype / scalar reconstructors and nothing else (no arbitrary
+    callables), instead of np.load(allow_pickle=True)."""
+    import io
+    import pickle
+
+    allowed = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+               ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+               ("numpy", "ndarray"), ("numpy", "dtype")}
+
+    class Restricted(pickle.Unpickler):
+        def find_class(self, module, name):
+            if (module, name) not in allowed:
+                raise pickle.UnpicklingError(f"refused {module}.{name}")
+            return super().find_class(module, name)
+
+    with open(path, "rb") as fh:
+        version = np.lib.format.read_magic(fh)
+        shape, _, dtype = np.lib.format._read_array_header(fh, version)
+        assert dtype == np.dtype(object) and shape == ()
+        obj = Restricted(io.BytesIO(fh.read())).load()
+    return obj.item() if isinstance(obj, np.ndarray) else obj
+
+
 def test_reference_import_lines_resolve_here():
     """The import block of experiment_four_focal_spots.ipynb (cell 0) and the DONN / extend-DOF
     notebooks, after install_reference_aliases(): every name is this package's object."""
@@ -61,7 +86,7 @@ def test_doe_save_writes_the_reference_bytes(tmp_path, monkeypatch):
     got = open(f, "rb").read()
     ref = open(os.path.join(GOLDEN, "save_ref.bin"), "rb").read()
     assert len(got) == c["nbytes"] and got == ref
-    d = np.load(f, allow_pickle=True).item()  # this file was written by our own code
+    d = _load_npy_dict_restricted(f)
     assert d["thickness"].shape == tuple(c["crop"]) and float(d["dxy"]) == c["doe_params"]["doe_dxy"]
 
 
@@ -106,3 +131,19 @@ def test_doe_xyz_coordinates_export(tmp_path, monkeypatch, capsys):
     assert out[0].startswith("The physical length of hologram is") and out[1] == "6"
     lin = DOE_xyz_cordinates_Generator(h, 2e-3, new_dxy=1e-3, interp="linear")
     assert lin[:, 2].min() >= h.min() - 1e-15 and lin[:, 2].max() <= h.max() + 1e-15
+
+
+def test_asm_forward_refuses_multi_valued_z():
+    """ASM_prop.forward propagates one z (the reference's transfer function does not give one plane
+    per value of a multi-valued z, Props/ASM_Prop.py:253): several values raise ValueError naming
+    propagate_planes instead of silently propagating z[0].  Raised before any device work."""
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    f = ElectricField(torch.zeros(1, 1, 8, 8, dtype=torch.complex64), wavelengths=1e-3, spacing=1e-3,
+                      device=torch.device("cpu"))
+    prop = ASM_prop(z_distance=torch.tensor([0.1, 0.2]), device=torch.device("cpu"))
+    with pytest.raises(ValueError, match="propagate_planes"):
+        prop(f)
+    prop.z = [0.3, 0.4, 0.5]
+    with pytest.raises(ValueError, match="propagate_planes"):
+        prop(f)

@@ -1,0 +1,74 @@
+"""Deterministic end-to-end golden: designed 4-level height maps through the
+whole four-focal-spots system -- Guassian_beam -> ASM 127 mm -> thin lens -> 80 mm aperture ->
+FixDOEElement(tolerance = 0) -> ASM 200 mm -> MSE(normalize(|E|^2), nine-PSF target) -- written
+with the notebook's own import lines (experiment_four_focal_spots.ipynb:198-260), vs the
+REFERENCE's own run of the same system (tests/golden/e2e_golden.npz, gen_e2e_golden.py, fp64 by
+the SURVEY §8(c) procedure).
+
+The reference's designed maps (edoe_4levels.npy, plot_data/example_1/splitter_*.npy) are pickled
+object arrays that are never unpickled here (gen_e2e_golden.py); the maps are designed 4-level
+splitters of the same kind (an 80 x 80 map upsampled to the 100 x 100 field, and a 100 x 100 one).
+
+Tolerances: the field before the DOE and the detector field rel-L2 <= 1e-4 (SURVEY §8(c) ASM
+bound; the reference's own fp32 error here is 5e-5), the loss within 1e-4 relative, the height-map
+gradient (d loss / d h through the modulation and the ASM adjoint) within 1e-3 rel-L2.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_io import GOLDEN, rel_l2
+
+pytestmark = pytest.mark.gpu
+
+with open(os.path.join(GOLDEN, "e2e_manifest.json")) as _fh:
+    E2E = json.load(_fh)
+
+
+def _arrays():
+    with np.load(os.path.join(GOLDEN, "e2e_golden.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("case", E2E["cases"], ids=[c["name"] for c in E2E["cases"]])
+def test_designed_doe_through_four_focal_spots_system(case):
+    import quantizationawarethzdoe_amd as pkg
+    pkg.install_reference_aliases()
+    import torch.nn as nn
+    from Components.Aperture import ApertureElement
+    from Components.QuantizedDOE import FixDOEElement
+    from Components.Thin_Lens import Thin_LensElement
+    from LightSource.Gaussian_beam import Guassian_beam
+    from Props.ASM_Prop import ASM_prop
+    from utils.Helper_Functions import normalize
+    from utils.units import m, mm
+
+    A = _arrays()
+    k = case["name"]
+    eps, tand = E2E["material"]
+    wavelengths = 2.998e8 / (E2E["f_ghz"] * 1e9)
+    source = Guassian_beam(height=100, width=100, beam_waist_x=None, beam_waist_y=None, wavelengths=wavelengths,
+                           spacing=1 * mm)
+    asm_prop1 = ASM_prop(z_distance=0.127 * m, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True)
+    lens = Thin_LensElement(focal_length=0.127 * m)
+    aperture = ApertureElement(aperture_type='rect', aperture_size=0.08)
+    field_in = aperture(lens(asm_prop1(source())))
+    assert rel_l2(field_in.data.detach().cpu().numpy(), A["field_in64"]) <= 1e-4
+
+    doe = FixDOEElement(height_map=torch.from_numpy(A[f"{k}__h"]), tolerance=0.0, material=[eps, tand])
+    asm_prop3 = ASM_prop(z_distance=200 * mm, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True)
+    out = asm_prop3(doe(field_in))
+    target = torch.from_numpy(A["target32"]).to(out.data.device)
+    loss = nn.MSELoss()(normalize(torch.abs(out.data) ** 2), target)
+    loss.backward()
+
+    e_out = rel_l2(out.data.detach().cpu().numpy(), A[f"{k}__out64"])
+    assert e_out <= 1e-4, e_out
+    ref_loss = float(A[f"{k}__loss64"])
+    assert abs(float(loss.detach()) - ref_loss) <= 1e-4 * ref_loss, (float(loss.detach()), ref_loss)
+    g = doe.height_map.grad.detach().cpu().numpy()
+    e_g = rel_l2(g, A[f"{k}__grad64"])
+    assert e_g <= 1e-3, e_g

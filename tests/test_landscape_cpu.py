@@ -52,9 +52,14 @@ def test_landscape_matches_direct_evaluation(tmp_path):
     model = _Toy()
     w0 = [p.data.clone() for p in model.parameters()]
     dirs = create_random_directions(model, generator=torch.Generator().manual_seed(1))
-    # filter-normalised: |d| = |w| per tensor, 1-d parameters get zero
+    # filter-normalised as the reference's normalize_direction(d, w) (VisTools/directions.py:102-111):
+    # each slice along dim 0 of d has the norm of the matching slice of w, 1-d parameters get zero
     for d, w in zip(dirs[0], w0):
-        assert abs(float(d.norm()) - (float(w.norm()) if w.dim() > 1 else 0.0)) <= 1e-5 * (1 + float(w.norm()))
+        if w.dim() <= 1:
+            assert float(d.abs().max()) == 0.0
+            continue
+        for dr, wr in zip(d, w):
+            assert abs(float(dr.norm()) - float(wr.norm())) <= 1e-5 * (1 + float(wr.norm()))
     target = torch.rand(1, 1, 6, 5, generator=torch.Generator().manual_seed(2))
     path = calulate_single_element_loss_landscape(_args(), model, target, directions=dirs, save_path=str(tmp_path))
     x, y, loss = load_surface(path)

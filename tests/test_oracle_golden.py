@@ -334,3 +334,37 @@ def test_asm_oracle_multi_plane_cfg2_matches_reference():
             assert rel_l2(y[2048], G[f"p{p}__row32"]) <= 1e-6
             e = float(np.sum(np.abs(y) ** 2))
             assert abs(e - float(G[f"p{p}__energy32"])) <= 1e-6 * e
+
+
+def _e2e():
+    import json
+    import os
+    from tests.golden_io import GOLDEN
+    with open(os.path.join(GOLDEN, "e2e_manifest.json")) as fh:
+        man = json.load(fh)
+    with np.load(os.path.join(GOLDEN, "e2e_golden.npz"), allow_pickle=False) as z:
+        return man, {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("name", ["splitter4_80", "splitter9_100"])
+def test_e2e_designed_doe_oracle_matches_reference(name):
+    """The deterministic end-to-end golden (tests/golden/gen_e2e_golden.py): the oracle's composition
+    of the four-focal-spots system with a FixDOE (tolerance 0) reproduces the reference's fp32 run:
+    field, loss and height-map gradient."""
+    man, A = _e2e()
+    lam = wavelengths([man["f_ghz"]])
+    d = torch.tensor(1e-3, dtype=torch.float32)
+    sp = torch.tensor([1e-3, 1e-3], dtype=torch.float32)
+    src = orc.gaussian_beam(100, 100, d, d, lam)
+    f1 = orc.asm_forward(src, lam, sp, 0.127, padding_scale=2)
+    f3 = orc.thin_lens(f1, d, d, 0.127, lam) * orc.aperture_mask(100, 100, d, d, "rect", 0.08)[None, None]
+    assert rel_l2(f3.numpy(), A["field_in32"]) <= 1e-5
+    h = torch.from_numpy(A[f"{name}__h"]).requires_grad_(True)
+    mat = torch.tensor(man["material"])
+    fm = orc.doe_modulate(f3, h, lam, mat[0], mat[1], tolerance=0.0, noise_u01=torch.zeros_like(h))
+    out = orc.asm_forward(fm, lam, sp, 0.2, padding_scale=2)
+    assert rel_l2(out.detach().numpy(), A[f"{name}__out32"]) <= 1e-5
+    loss = orc.intensity_mse(out, torch.from_numpy(A["target32"]))
+    assert abs(float(loss) - float(A[f"{name}__loss32"])) <= 1e-5 * float(A[f"{name}__loss32"])
+    loss.backward()
+    assert rel_l2(h.grad.numpy(), A[f"{name}__grad32"]) <= 1e-4
