@@ -12,9 +12,12 @@
 // Forward schedule 16 (L=1), 16 (L=16), 4 (L=256): the result X[j], j = i + 256 q, sits in lane
 // i % 64 as reg[i / 64][q] (i < 256, q < 4).  The inverse starts with radix 4 on exactly those
 // registers, then 16 (L=4), 16 (L=64): output j = lane + 64 q, q < 16.
-// Twiddles: per workgroup in LDS (shared by its waves), exp(-2 pi i t / n) for n = 1024, 256 and 64
-// (TAB entries): each stage reads its own table at k r, which keeps a stage's 16 distinct k of a
-// 32-lane group on distinct banks.
+// Twiddles: per workgroup in LDS (shared by its waves), one table per read pattern so that every
+// twiddle read of a 32-lane group is conflict-free (ds_read_b64, bank = dword mod 64; the model is
+// scripts/wfft_bank_sim.py): w1024^t (t < 768: the forward's last stage reads k and 3k, odd strides),
+// w1024^(2k) (k < 256), w256^(r k) as a 16 x 16 [r][k] table, w64^t, and the inverse's last stage
+// w1024^(lane r) as a 15 x 64 [r - 1][lane] table (the flat w1024^(lane r) put 2 to 8 distinct
+// slots on one bank for even r).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -25,17 +28,26 @@ namespace wf {
 
 constexpr int N = 1024;
 constexpr int LANES = 64;
-constexpr int IMG = N + N / 32;  // floats per wave image: pad(j) = j + j / 32
-constexpr int TAB = 1024 + 256 + 64;  // float2 twiddle entries per workgroup
+constexpr int IMG = N + 2 * (N / 32);  // floats per wave image: pad2(1023) = 1023 + 2 * 31
+constexpr int T1024 = 0, T512 = 768, T256 = 1024, T64 = 1280, TINV = 1344;
+constexpr int TAB = TINV + 15 * 64;  // float2 twiddle entries per workgroup
 struct Tabs {
-  const float2* t1024;
-  const float2* t256;
-  const float2* t64;
+  const float2* t1024;  // w1024^t, t < 768
+  const float2* t512;   // w1024^(2 k), k < 256
+  const float2* t256;   // [r][k] = w256^(r k)
+  const float2* t64;    // w64^t
+  const float2* tinv;   // [r - 1][lane] = w1024^(lane r)
 };
-// image padding: every read pattern of the schedule (x[lane + 64 r] and x[lane + 64 m + 256 r]) is
-// conflict-free on the 32 banks of ds_read_b32 and every write pattern at most 2-way (free on
-// ds_write_b32; MI355X_MICROARCH.md §LDS)
+// image padding, one per exchange (the write and the read of an exchange share it):
+// pad1(j) = j + (j >> 5) for the first exchange of either transform, pad2(j) = j + 2 (j >> 5) for the
+// second.  Every read pattern (x[lane + 64 r], x[lane + 64 m + 256 r]) walks 32 consecutive
+// elements of one 32-aligned run, so any such pad keeps it conflict-free on the 32 banks of
+// ds_read_b32; the writes need the slope: the forward's second exchange writes 16-element runs of
+// two 256-apart groups (pad1 folds them 8 banks apart, a 2-way conflict on every write), the
+// inverse's writes runs of 4 lanes 64 apart (pad2 spreads them over all 32 banks).
+// (MI355X_MICROARCH.md §LDS; scripts/wfft_bank_sim.py)
 __device__ __forceinline__ int pad(int j) { return j + (j >> 5); }
+__device__ __forceinline__ int pad2(int j) { return j + 2 * (j >> 5); }
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -45,15 +57,18 @@ __device__ __forceinline__ void wave_sync() {
 
 // the workgroup's twiddle tables (all threads; barrier before use): every entry is a root of the
 // 1024-point plan table tw1024[t] = exp(-2 pi i t / 1024) (fp64-rounded on the host), gathered
-// from L2 -- w256^e = tw1024[4 e], w64^e = tw1024[16 e]
+// from L2 -- w1024^(2k) = tw1024[2 k], w256^e = tw1024[4 e], w64^e = tw1024[16 e]
+__device__ __forceinline__ int tab_source(int t) {
+  if (t < T512) return t;                                        // w1024^t
+  if (t < T256) return 2 * (t - T512);                           // w1024^(2 k)
+  if (t < T64) return 4 * ((t - T256) >> 4) * ((t - T256) & 15);  // [r][k] = w256^(r k)
+  if (t < TINV) return 16 * (t - T64);                           // w64^t
+  const int q = t - TINV;                                        // [r - 1][lane] = w1024^(lane r)
+  return (q & 63) * ((q >> 6) + 1);
+}
 __device__ __forceinline__ Tabs fill_tables(float2* tab, const float2* __restrict__ tw1024, int tid, int nt) {
-  // t256 as a 16 x 16 table [r][k] = w256^(r k): stage 1's 16 butterflies k read 16 consecutive
-  // slots per r (the flat w256^(k r) put 2 to 4 distinct slots on one bank for r = 4, 8, 12)
-  for (int t = tid; t < TAB; t += nt) {
-    const int q = t - 1024;
-    tab[t] = tw1024[t < 1024 ? t : (t < 1280 ? 4 * (q >> 4) * (q & 15) : 16 * (t - 1280))];
-  }
-  return Tabs{tab, tab + 1024, tab + 1280};
+  for (int t = tid; t < TAB; t += nt) tab[t] = tw1024[tab_source(t)];
+  return Tabs{tab + T1024, tab + T512, tab + T256, tab + T64, tab + TINV};
 }
 
 // This wave's float image behind the workgroup's tables.  Its offset is made opaque so the
@@ -107,18 +122,21 @@ __device__ __forceinline__ void forward(float* img, const Tabs& tw, int lane, Ld
   for (int r = 1; r < 16; ++r) x1[r] = cmul(x1[r], tw.t256[16 * r + k1]);
   dft16<false>(x1);
   // outputs y[(i - k) 16 + k + 16 q] -> stage 2 inputs x[i2 + 256 r], i2 = lane + 64 m
-  // pad((lane - k) 16 + k + 16 q) = (lane - k) 16 + k + 8 (lane >> 4) + 16 q + (q >> 1)
+  // pad2((lane - k) 16 + k + 16 q) = (lane - k) 16 + k + 16 (lane >> 4) + 16 q + 2 (q >> 1);
+  // pad2(lane + 64 r) = pad2(lane) + 68 r
   float2 x2[16];
-  const int w1 = (lane - k1) * 16 + k1 + 8 * (lane >> 4);
-  exchange(img, x1, [&](int q) { return w1 + 16 * q + (q >> 1); }, x2,
-           [&](int b) { return pl + 66 * ((b >> 2) + 4 * (b & 3)); });
-  // stage 2: radix 4, L = 256, k = i2: twiddle w1024^(k r)
+  const int w1 = (lane - k1) * 16 + k1 + 16 * (lane >> 4);
+  const int pl2 = pad2(lane);
+  exchange(img, x1, [&](int q) { return w1 + 16 * q + 2 * (q >> 1); }, x2,
+           [&](int b) { return pl2 + 68 * ((b >> 2) + 4 * (b & 3)); });
+  // stage 2: radix 4, L = 256, k = i2: twiddle w1024^(k r) (k and 3 k: odd strides; 2 k from its
+  // own table)
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
     const int k = lane + 64 * m;
     float2* q = &x2[4 * m];
     q[1] = cmul(q[1], tw.t1024[k]);
-    q[2] = cmul(q[2], tw.t1024[2 * k]);
+    q[2] = cmul(q[2], tw.t512[k]);
     q[3] = cmul(q[3], tw.t1024[3 * k]);
     dft4<false>(q[0], q[1], q[2], q[3]);
 #pragma unroll
@@ -144,13 +162,16 @@ __device__ __forceinline__ void inverse(float* img, const Tabs& tw, int lane, fl
   for (int r = 1; r < 16; ++r) x1[r] = cmulc(x1[r], tw.t64[k1 * r]);
   dft16<true>(x1);
   // outputs y[(i - k) 16 + k + 4 q] -> stage 2 inputs x[lane + 64 r]
-  // pad((lane - k) 16 + k + 4 q) = (lane - k) 16 + k + 2 (lane >> 2) + 4 q + (q >> 3)
+  // pad2((lane - k) 16 + k + 4 q) = (lane - k) 16 + k + 4 (lane >> 2) + 4 q + 2 (q >> 3);
+  // pad2(lane + 64 r) = pad2(lane) + 68 r
   float2 x2[16];
-  const int w1 = (lane - k1) * 16 + k1 + 2 * (lane >> 2);
-  exchange(img, x1, [&](int q) { return w1 + 4 * q + (q >> 3); }, x2, [&](int r) { return pl + 66 * r; });
-  // stage 2: radix 16, L = 64, k = lane: conj twiddle w1024^(k r); outputs y[lane + 64 q]
+  const int w1 = (lane - k1) * 16 + k1 + 4 * (lane >> 2);
+  const int pl2 = pad2(lane);
+  exchange(img, x1, [&](int q) { return w1 + 4 * q + 2 * (q >> 3); }, x2, [&](int r) { return pl2 + 68 * r; });
+  // stage 2: radix 16, L = 64, k = lane: conj twiddle w1024^(k r) from the [r - 1][lane] table;
+  // outputs y[lane + 64 q]
 #pragma unroll
-  for (int r = 1; r < 16; ++r) x2[r] = cmulc(x2[r], tw.t1024[lane * r]);
+  for (int r = 1; r < 16; ++r) x2[r] = cmulc(x2[r], tw.tinv[64 * (r - 1) + lane]);
   dft16<true>(x2);
 #pragma unroll
   for (int q = Q0; q < 16; ++q) sv(q, lane + 64 * q, x2[q]);
