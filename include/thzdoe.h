@@ -66,8 +66,10 @@ int thz_abi_version(void);
  * Angular-spectrum propagation, Props/ASM_Prop.py:314-378 (forward) and its
  * adjoint (autograd backward, == ASM with conj(H)).
  *
- * Forward : in  [B, C, H, W]            -> out [Z, B, C, Ho, Wo]
- * Adjoint : in  [Z, B, C, Ho, Wo] (Z==1) -> out [B, C, H, W]
+ * Forward : in  [B, C, H, W]     -> out [Z, B, C, Ho, Wo]
+ * Adjoint : in  [Z, B, C, Ho, Wo] -> out [B, C, H, W] = sum over z of plane z's adjoint (the
+ *           autograd backward of a Z-plane forward; the column pass sums the planes' spectra,
+ *           one inverse column transform and one row pass in all)
  * with Ho = H, Wo = W when unpad != 0 (CenterCrop, :359-361) else Ho = H+2 pad_h,
  * Wo = W + 2 pad_w (do_unpad_after_pad=False).  pad_h = floor(s_h H / 2) as in
  * compute_padding (:119-136); do_padding=False is pad_h = pad_w = 0.
@@ -79,7 +81,7 @@ typedef struct thz_asm_desc {
   int unpad;
   int bandlimit;            /* THZ_BANDLIMIT_* */
   int Z;                    /* 1 .. THZ_MAX_Z */
-  int adjoint;              /* 0 forward, 1 adjoint (requires Z == 1) */
+  int adjoint;              /* 0 forward, 1 adjoint (sums the Z planes) */
   int z_chunk;              /* z-planes per column pass; 0 = library default */
   float dx, dy;
   const float* wavelengths; /* host [C] */
@@ -87,7 +89,8 @@ typedef struct thz_asm_desc {
 } thz_asm_desc;
 
 /* Workspace: the row-pass spectrum T [BC][ncols][H], one z-chunk of column-pass output
- * U [zc][BC][ncols][Ho] (both complex64), and for a 300-point padded height the
+ * U [zc][BC][ncols][Ho] (both complex64; the adjoint holds a z-chunk of input planes in T,
+ * [zc][BC][ncols][Ho], and one summed plane in U), and for a 300-point padded height the
  * mixed-radix column pass's per-(wavelength, column) tables (sqrt row values and
  * kept-row bounds).  Contents need not persist between calls. */
 int thz_asm_workspace_size(const thz_asm_desc* d, size_t* bytes);

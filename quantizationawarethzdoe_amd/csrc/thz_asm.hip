@@ -51,6 +51,11 @@ struct AsmArgs {
   int nz, zoff;                   // z-planes in this chunk, offset into zv
   int kfull, kparts;              // K2 tasks: kfull whole columns, then the rest split in kparts z-ranges
   int bl, adjoint;
+  // adjoint over Z planes in one pipeline (autograd backward of a multi-plane forward): K1 runs
+  // over the chunk's nz input planes (T holds nz planes), K2 sums FFT(T_z) conj(H_z) over them
+  // into one spectrum per column and inverts once (zacc: add into U, for the chunks after the
+  // first), K3 runs once on the single summed plane
+  int zsum, zacc;
   float dx, dy, scale;
   const float2* tft;  // RSC: column-major transfer-function table [C][ncols][Ph] (nullptr: analytic ASM)
   int vec;            // VRS: plane b == 2 is Ez = (Ex x + Ey y) / r computed in the row pass
@@ -207,9 +212,12 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
     }
   }
   const int row = xcd_rows(blockIdx.x, nrows);
-  const int bc = row / a.Hin, h = row - bc * a.Hin;
-  const float2* src = in + ((size_t)bc * a.Hin + h) * a.Win;
-  float2* dst = T + (size_t)bc * a.ncb * CB * a.Hin;
+  // plane = zz * BC + bc: one plane (zz = 0) except in the Z-summing adjoint, whose chunk's input
+  // planes start at plane zoff * BC of `in`
+  const int plane = row / a.Hin, h = row - plane * a.Hin;
+  const int bc = plane % a.BC;
+  const float2* src = in + ((size_t)((a.zsum ? a.zoff * a.BC : 0) + plane) * a.Hin + h) * a.Win;
+  float2* dst = T + (size_t)plane * a.ncb * CB * a.Hin;
   // VRS (Props/RSC_Prop.py:294-303): plane b = 2 is Ez = Ex x / r + Ey y / r on the unpadded
   // grid linspace(-N dx/2, N dx/2, N) (dx on both axes, :83-84)
   const bool ez = a.vec && bc / a.C == 2;
@@ -334,8 +342,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
-    fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tid, ld0, sv0);
-    if (!a.tft) {
+    if (!a.zsum) fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tid, ld0, sv0);
+    if (!a.tft && !a.zsum) {
       // 1 / (Ph Pw) is a power of two: scaling the spectrum once per column instead of every
       // output plane is exact
 #pragma unroll
@@ -395,6 +403,46 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
         sq[m][r] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
       }
     __syncthreads();  // mz visible
+    if (a.zsum) {
+      // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
+#pragma unroll
+      for (int m = 0; m < MBL; ++m)
+#pragma unroll
+        for (int r = 0; r < RL; ++r) sp[m][r] = make_float2(0.f, 0.f);
+      for (int zz = z_lo; zz < z_hi; ++zz) {
+        const float z = a.zv[a.zoff + zz];
+        const int M = mz[zz - z_lo];
+        const float2* colz = T + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
+        int tz = threadIdx.x;
+        asm volatile("" : "+v"(tz));
+        auto ldz = [&](int, int, int idx) {
+          const int s = idx - a.in_r0;
+          return (s >= 0 && s < a.Hin) ? colz[(size_t)s * CB] : make_float2(0.f, 0.f);
+        };
+        auto acc = [&](int m, int r, int j, float2 v) {
+          const int mx = freq_index(j, PN);
+          if (mx > M || -mx > M) return;
+          float sn, cs;
+          sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
+          sp[m][r] = cadd(sp[m][r], cmul(v, make_float2(cs, -sn)));
+        };
+        fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tz, ldz, acc);
+      }
+#pragma unroll
+      for (int m = 0; m < MBL; ++m)
+#pragma unroll
+        for (int r = 0; r < RL; ++r) sp[m][r] = cscale(sp[m][r], a.scale);
+      int tz = threadIdx.x;
+      asm volatile("" : "+v"(tz));
+      auto ld1 = [&](int m, int r, int) { return sp[m][r]; };
+      float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      auto sv1 = [&](int, int, int j, float2 v) {
+        const int r = j - a.out_r0;
+        if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = a.zacc ? cadd(dst[(size_t)r * CBU], v) : v;
+      };
+      fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
+      return;
+    }
     for (int zz = z_lo; zz < z_hi; ++zz) {
       const float z = a.zv[a.zoff + zz];
       const int M = mz[zz - z_lo];
@@ -424,6 +472,46 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
     }
   } else {
+    if (a.zsum) {
+      // adjoint over the chunk's planes (see the power-of-two branch)
+      float2 acc[FFT_MAXV];
+#pragma unroll
+      for (int m = 0; m < FFT_MAXV; ++m) acc[m] = make_float2(0.f, 0.f);
+      for (int zz = z_lo; zz < z_hi; ++zz) {
+        const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+        const float2* colz = T + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
+        int tm = threadIdx.x;
+        asm volatile("" : "+v"(tm));
+        __syncthreads();  // the previous plane's readers are done with lds
+        for (int i = tm; i < Ph; i += nt) {
+          const int si = i - a.in_r0;
+          lds[padx(i)] = (si >= 0 && si < a.Hin) ? colz[(size_t)si * CB] : make_float2(0.f, 0.f);
+        }
+        __syncthreads();
+        fft_lds<false>(lds, ph, tm, nt);
+#pragma unroll
+        for (int m = 0; m < FFT_MAXV; ++m) {
+          const int i = tm + m * nt;
+          if (i < Ph) acc[m] = cadd(acc[m], cmul(lds[padx(i)], tf_value(a, s, kfreq(freq_index(i, Ph), Ph, a.dx), Ky)));
+        }
+      }
+      int tm = threadIdx.x;
+      asm volatile("" : "+v"(tm));
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < FFT_MAXV; ++m) {
+        const int i = tm + m * nt;
+        if (i < Ph) lds[padx(i)] = acc[m];
+      }
+      __syncthreads();
+      fft_lds<true>(lds, ph, tm, nt);
+      float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      for (int r = tm; r < a.Hout; r += nt) {
+        const float2 v = cscale(lds[padx(a.out_r0 + r)], a.scale);
+        dst[(size_t)r * CBU] = a.zacc ? cadd(dst[(size_t)r * CBU], v) : v;
+      }
+      return;
+    }
     for (int i = tid; i < Ph; i += nt) {
       const int s = i - a.in_r0;
       lds[padx(i)] = (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
@@ -543,7 +631,7 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
   };
   auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
   const auto twr = MP::template twiddles<MX_T>(ph.tw, tid);
-  MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
+  if (!a.zsum) MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
   if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
     const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
     int tz = threadIdx.x;
@@ -571,6 +659,45 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
     const int i = tid + m * MX_T;
 #pragma unroll
     for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
+  }
+  if (a.zsum) {
+    // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
+#pragma unroll
+    for (int m = 0; m < MBL; ++m)
+#pragma unroll
+      for (int r = 0; r < RL; ++r) sp[m][r] = make_float2(0.f, 0.f);
+    for (int zz = z_lo; zz < z_hi; ++zz) {
+      const float z = a.zv[a.zoff + zz];
+      const int M = mzc[zz];
+      const float2* colz = T + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
+      int tz = threadIdx.x;
+      asm volatile("" : "+v"(tz));
+      auto ldz = [&](int, int, int idx) {
+        const int s = idx - a.in_r0;
+        return (s >= 0 && s < a.Hin) ? colz[(size_t)s * CB] : make_float2(0.f, 0.f);
+      };
+      auto acc = [&](int m, int r, int j, float2 v) {
+        const int mx = freq_index(j, PN);
+        if (mx > M || -mx > M) return;
+        float sn, cs;
+        sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
+        sp[m][r] = cadd(sp[m][r], cmul(v, make_float2(cs, -sn)));
+      };
+      MP::template run<false, MX_T>(lds, twr, tz, ldz, acc);
+    }
+    int tz = threadIdx.x;
+    asm volatile("" : "+v"(tz));
+    auto ld1 = [&](int m, int r, int) { return sp[m][r]; };
+    float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+    auto sv1 = [&](int, int, int j, float2 v) {
+      const int r = j - a.out_r0;
+      if ((unsigned)r < (unsigned)a.Hout) {
+        const float2 o = cscale(v, a.scale);
+        dst[(size_t)r * CBU] = a.zacc ? cadd(dst[(size_t)r * CBU], o) : o;
+      }
+    };
+    MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
+    return;
   }
   for (int zz = z_lo; zz < z_hi; ++zz) {
     const float z = a.zv[a.zoff + zz];
@@ -782,6 +909,7 @@ __global__ void __launch_bounds__(1024) fft_rows_kernel(const float2* __restrict
 struct AsmGeom {
   int BC, Ph, Pw, ncols, J, ncb, ncbu, Hin, Win, Hout, Wout, zc;
   int C;
+  int adj;  // adjoint: T holds the z-chunk's planes, U one (summed) plane
 };
 
 static int validate(const thz_asm_desc* d) {
@@ -790,7 +918,6 @@ static int validate(const thz_asm_desc* d) {
     return fail(THZ_E_ARG, "bad shape B=%d C=%d H=%d W=%d pad=(%d,%d)", d->B, d->C, d->H, d->W, d->pad_h, d->pad_w);
   if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d wavelengths", d->C, THZ_MAX_WAVELENGTHS);
   if (d->Z < 1 || d->Z > THZ_MAX_Z) return fail(THZ_E_UNSUPPORTED, "Z=%d outside [1, %d]", d->Z, THZ_MAX_Z);
-  if (d->adjoint && d->Z != 1) return fail(THZ_E_ARG, "adjoint needs Z == 1 (got %d)", d->Z);
   if (d->bandlimit < 0 || d->bandlimit > 2) return fail(THZ_E_ARG, "bad bandlimit %d", d->bandlimit);
   if (!d->wavelengths || !d->z) return fail(THZ_E_ARG, "null wavelengths / z");
   if (!(d->dx > 0.f) || !(d->dy > 0.f)) return fail(THZ_E_ARG, "spacing must be > 0");
@@ -859,10 +986,13 @@ static void geometry(const thz_asm_desc* d, AsmGeom* g) {
     // default: up to 64 z-planes per column pass (the forward column FFT and the T read are
     // shared by the chunk; one K2 and one K3 launch per 64 planes), U capped at 10 GiB of the
     // 288 GB HBM.  Measured on cfg2 (64 planes, round 2): z_chunk 32 / 64 -> 6830 / 7270 planes/s.
-    const double per_z = (double)g->BC * g->ncbu * CBU * g->Hout * sizeof(float2);
+    // The Z-summing adjoint keeps the chunk's input planes in T instead (same cap).
+    const double per_z = d->adjoint ? (double)g->BC * g->ncb * CB * g->Hin * sizeof(float2)
+                                    : (double)g->BC * g->ncbu * CBU * g->Hout * sizeof(float2);
     zc = (int)std::max(1.0, std::min(64.0, std::floor((10240.0 * 1024 * 1024) / per_z)));
   }
-  g->zc = std::min(zc, d->adjoint ? 1 : d->Z);
+  g->zc = std::min(zc, d->Z);
+  g->adj = d->adjoint;
 }
 
 // Compile-time power-of-two instantiations (blockDim = n / FFT_MAXV); 0 = runtime plan.
@@ -976,9 +1106,61 @@ static size_t tab_sq_bytes(const AsmGeom& g) { return align256((size_t)g.C * g.n
 static size_t tab_bytes(const AsmGeom& g) {
   return mx_kind(g.Ph) ? tab_sq_bytes(g) + align256((size_t)g.C * g.ncols * g.zc * sizeof(int)) : 0;
 }
+static size_t t_bytes(const AsmGeom& g) {
+  return align256((size_t)(g.adj ? g.zc : 1) * g.BC * g.ncb * CB * g.Hin * sizeof(float2));
+}
 static size_t ws_bytes(const AsmGeom& g) {
-  return align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)) +
-         align256((size_t)g.zc * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2)) + tab_bytes(g);
+  return t_bytes(g) + align256((size_t)(g.adj ? 1 : g.zc) * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2)) +
+         tab_bytes(g);
+}
+
+// The adjoint of a Z-plane forward (sum over planes): per z-chunk, K1 over the chunk's input
+// planes and the Z-summing K2 (adding into U after the first chunk); then K3 once.
+static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
+                           hipStream_t s, FftPlan pw, FftPlan ph, bool mx_tabs) {
+  a.zsum = 1;
+  a.tab_blocks = 0;
+  a.kfull = g.ncols * g.BC;  // every column task runs all of its chunk's planes
+  a.kparts = 1;
+  const int th = threads_for(g.Ph);
+  for (int z0 = 0; z0 < Z; z0 += g.zc) {
+    a.zoff = z0;
+    a.nz = std::min(g.zc, Z - z0);
+    a.zacc = z0 > 0;
+    {
+      KernelTimer kt("asm_rows_fwd", s);
+      THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(a.nz * g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in, T,
+                      pw, a);
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+    {
+      KernelTimer kt("asm_cols", s);
+      if (mx_kind(g.Ph) == Mx300::N) {
+        if (mx_tabs) {
+          hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
+          THZ_LAUNCH_CHECK();
+        }
+        const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
+        hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+      } else {
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(a.kfull), dim3(th), lds2, s, (const float2*)T, U, ph, a);
+      }
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+  }
+  a.zoff = 0;
+  a.nz = 1;
+  {
+    KernelTimer kt("asm_rows_inv", s);
+    THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
+                    (float2*)out, pw, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  return THZ_OK;
 }
 
 // K1 once, then (K2, K3) per z-chunk, on a prepared argument block.
@@ -993,6 +1175,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     a.sqt = (float*)tabs;
     a.mzt = (int*)(tabs + tab_sq_bytes(g));
   }
+  if (g.adj && Z > 1) return run_adjoint_sum(a, g, Z, in, out, T, U, s, pw, ph, mx_tabs);
   // square mixed-radix grids (cfg4 / cfg5): the first z-chunk's column tables ride along with K1
   a.tab_blocks = mx_tabs && mx_kind(g.Pw) == Mx300::N ? g.C * g.ncols : 0;
   {
@@ -1136,7 +1319,7 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
   }
 
   float2* T = (float2*)workspace;
-  float2* U = (float2*)((char*)workspace + align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2)));
+  float2* U = (float2*)((char*)workspace + t_bytes(g));
   char* tabs = (char*)workspace + ws_bytes(g) - tab_bytes(g);
   return run_pipeline(a, g, d->Z, in, out, T, U, (hipStream_t)stream, pw, ph, tab_bytes(g) ? tabs : nullptr);
 }
@@ -1255,6 +1438,8 @@ static int rsc_plan(const thz_rsc_desc* d, RscPlan* p) {
   g.ncb = (g.ncols + CB - 1) / CB;
   g.ncbu = (g.ncols + CBU - 1) / CBU;
   g.zc = 1;
+  g.adj = 0;
+  g.C = d->C;
   RscKArgs& k = p->k;
   k.C = d->C;
   k.Ph = g.Ph;

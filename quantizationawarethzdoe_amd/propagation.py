@@ -70,7 +70,9 @@ def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, 
 
 def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint=False, z_chunk=0,
               out=None):
-    """Raw launch: forward data [B,C,H,W] -> [Z,B,C,Ho,Wo]; adjoint [1,B,C,Ho,Wo] -> [B,C,H,W]."""
+    """Raw launch: forward data [B,C,H,W] -> [Z,B,C,Ho,Wo]; adjoint [Z,B,C,Ho,Wo] -> [B,C,H,W], the sum
+    over the Z planes of each plane's adjoint (one pipeline: the column pass sums the planes'
+    spectra, thz_asm_forward with adjoint = 1)."""
     _require_device(data, "ASM")
     if data.dtype != torch.complex64:
         raise TypeError(f"ASM kernels compute in complex64; got {data.dtype}")
@@ -78,8 +80,8 @@ def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, ad
     data = data.contiguous()
     if adjoint:
         Z, B, C, Ho, Wo = data.shape
-        if Z != 1:
-            raise ValueError("adjoint takes a single z-plane")
+        if Z != len(zs):
+            raise ValueError(f"adjoint: {Z} gradient planes for {len(zs)} z values")
         H = Ho - (0 if unpad else 2 * pad_h)
         W = Wo - (0 if unpad else 2 * pad_w)
         out_shape = (B, C, H, W)
@@ -121,11 +123,8 @@ class _AsmFunction(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
-        g = g.contiguous()
-        gin = None
-        for k, z in enumerate(zs):
-            gk = asm_apply(g[k:k + 1], wavelengths, spacing, [z], pad_h, pad_w, unpad, bandlimit, True)
-            gin = gk if gin is None else gin + gk
+        # one adjoint launch for all planes: sum_z A_z^H g_z, the sum taken in the column pass
+        gin = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
         return gin, None, None, None, None, None, None, None, None
 
 
@@ -138,8 +137,8 @@ def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, band
 
 class _AsmModulatedFunction(torch.autograd.Function):
     """ASM forward of DOELayer.modulate(field) in one pipeline (thz_asm_forward_modulated): the row
-    pass applies t_c(h + noise) in its loader.  Backward: the ASM adjoint per plane, then the
-    modulate backward kernel (grad_field, grad_height)."""
+    pass applies t_c(h + noise) in its loader.  Backward: the ASM adjoint summed over the planes
+    (one launch), then the modulate backward kernel (grad_field, grad_height)."""
 
     @staticmethod
     def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
@@ -176,11 +175,7 @@ class _AsmModulatedFunction(torch.autograd.Function):
         field, h = ctx.saved_tensors
         pend = ctx.pend
         wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
-        g = g.contiguous()
-        gm = None
-        for k, z in enumerate(zs):
-            gk = asm_apply(g[k:k + 1], wavelengths, spacing, [z], pad_h, pad_w, unpad, bandlimit, True)
-            gm = gk if gm is None else gm + gk
+        gm = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
         gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
                                         ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
         return gf, gh, None, None, None, None, None, None, None, None

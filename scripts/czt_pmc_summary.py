@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise scripts/r02_czt_close.sh output into profiles/: <tag>_czt_kernel_stats.csv (rocprofv3
+"""Summarise scripts/r03_czt.sh output into profiles/: <tag>_czt_kernel_stats.csv (rocprofv3
 --stats) and <tag>_czt_pmc_summary.json (per-kernel averages of every counter; hbm_bytes =
 (2 FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction of scripts/pmc_summary.py).
 usage: czt_pmc_summary.py <dir> <tag>"""
@@ -18,12 +18,14 @@ def main():
     prof = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles")
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_czt_kernel_stats.csv"))
     acc = {}
-    for f in sorted(glob.glob(os.path.join(src, "pmc", "g*", "**", "*counter_collection.csv"), recursive=True)):
+    for f in sorted(glob.glob(os.path.join(src, "pmc_*", "**", "*counter_collection.csv"), recursive=True)):
         for k, d in per_kernel(f).items():
             acc.setdefault(k, {}).update(d)
     for d in acc.values():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["hbm_bytes"] = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024
+        if d.get("SQ_INSTS_LDS"):
+            d["lds_bank_conflict_per_lds_inst"] = d.get("SQ_LDS_BANK_CONFLICT", 0) / d["SQ_INSTS_LDS"]
     with open(os.path.join(prof, f"{tag}_czt_pmc_summary.json"), "w") as f:
         json.dump(acc, f, indent=1)
     print(json.dumps({k: round(v.get("hbm_bytes", 0) / 1e6, 1) for k, v in acc.items()}))

@@ -351,3 +351,54 @@ def test_asm_largest_transform_p16384_properties():
     ex = float((x.abs().double() ** 2).sum())
     eax = float((ax.abs().double() ** 2).sum())
     assert 0.0 < eax <= ex * (1 + 1e-5), (eax, ex)
+
+
+@pytest.mark.parametrize("H,W,s,bl,C,Z,zc", [
+    (80, 72, 1.5, "approx", 2, 5, 0),       # runtime plan (P = 200 / 180), one chunk
+    (100, 100, 2, "exact", 1, 4, 0),        # P = 300: the mixed-radix column pass
+    (100, 100, 2, "exact", 1, 7, 3),        # P = 300, three chunks (the later ones add into U)
+    (512, 512, 1, "exact", 2, 5, 2),        # P = 1024: the power-of-two column pass, three chunks
+    (1024, 1024, 1, "exact", 1, 3, 0),      # P = 2048
+    (60, 70, 1, "none", 1, 3, 0),           # no band limit
+])
+def test_asm_multi_plane_backward_one_adjoint_vs_oracle(H, W, s, bl, C, Z, zc):
+    """The backward of a Z-plane forward is ONE adjoint launch that sums the planes' spectra in the
+    column pass (thz_asm_forward, adjoint = 1, Z > 1) -- vs autograd through the fp64 oracle's
+    per-plane forwards (rel-L2 <= 1e-4), through propagate_planes and through the raw C-ABI call
+    (with an explicit z_chunk so later chunks accumulate into U)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_padding
+    EF, ASM = _prop_cls()
+    dev = _dev()
+    rng = np.random.default_rng(H + Z + zc)
+    x = (rng.standard_normal((1, C, H, W)) + 1j * rng.standard_normal((1, C, H, W))).astype(np.complex64)
+    freqs = [300] if C == 1 else [260, 320]
+    wl = [C0 / (f * 1e9) for f in freqs]
+    dxy = 1.0 if H <= 100 else 0.5
+    zs = list(np.linspace(0.02, 0.12, Z) * (1 if H != 60 else 3))
+    g = (rng.standard_normal((Z, 1, C, H, W)) + 1j * rng.standard_normal((Z, 1, C, H, W))).astype(np.complex64)
+    xd = torch.from_numpy(x).to(dev).requires_grad_(True)
+    field = EF(xd, wavelengths=wl if C > 1 else wl[0], spacing=[dxy * 1e-3, dxy * 1e-3], device=dev)
+    prop = ASM(z_distance=zs[0], padding_scale=s, bandlimit_type="exact" if bl == "none" else bl,
+               bandlimit_kernel=bl != "none", device=dev)
+    planes = prop.propagate_planes(field, zs)
+    gx, = torch.autograd.grad(planes, xd, grad_outputs=torch.from_numpy(g).to(dev))
+    old = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        xo = torch.from_numpy(x).to(torch.complex128).requires_grad_(True)
+        lam = wavelengths(freqs, True)
+        sp = spacing(dxy, dxy, True)
+        outs = [orc.asm_forward(xo, lam, sp, z, s, bandlimit=bl != "none",
+                                bandlimit_type="exact" if bl == "none" else bl) for z in zs]
+        ref, = torch.autograd.grad(torch.stack(outs), xo, grad_outputs=torch.from_numpy(g).to(torch.complex128))
+    finally:
+        torch.set_default_dtype(old)
+    assert rel_l2(gx.cpu().numpy(), ref.numpy()) <= 1e-4, rel_l2(gx.cpu().numpy(), ref.numpy())
+    # the raw entry with an explicit chunk size: the same sum
+    ph, pw = asm_padding(H, W, (s, s))
+    code = {"exact": 1, "approx": 2, "none": 0}[bl]
+    sp32 = [float(np.float32(dxy * 1e-3))] * 2
+    wl32 = [float(np.float32(w)) for w in wl]
+    raw = asm_apply(torch.from_numpy(g).to(dev), wl32, sp32, zs, ph, pw, True, code, adjoint=True, z_chunk=zc)
+    assert raw.shape == (1, C, H, W)
+    assert rel_l2(raw.cpu().numpy(), ref.numpy()) <= 1e-4
