@@ -301,9 +301,11 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // ---------------------------------------------------------------------------------------------
 // K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
 // ---------------------------------------------------------------------------------------------
-template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
-                                                AsmArgs a) {
+// ZSUM: the Z-summing adjoint's column pass (a separate instantiation, so the forward's register
+// allocation is untouched by it)
+template <int PN, bool ZSUM>
+__device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                              AsmArgs a) {
   extern __shared__ float2 lds[];
   // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
   // resident-workgroup count), the last partial round's columns are split into kparts z-ranges
@@ -342,8 +344,8 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
     };
     auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
-    if (!a.zsum) fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tid, ld0, sv0);
-    if (!a.tft && !a.zsum) {
+    if constexpr (!ZSUM) fft_pow2_io<false, PN, TT, true, false, false>(lds, twl, tid, ld0, sv0);
+    if (!ZSUM && !a.tft) {
       // 1 / (Ph Pw) is a power of two: scaling the spectrum once per column instead of every
       // output plane is exact
 #pragma unroll
@@ -351,7 +353,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
 #pragma unroll
         for (int r = 0; r < RL; ++r) sp[m][r] = cscale(sp[m][r], a.scale);
     }
-    if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
+    if (!ZSUM && a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
@@ -403,7 +405,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
         sq[m][r] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
       }
     __syncthreads();  // mz visible
-    if (a.zsum) {
+    if constexpr (ZSUM) {
       // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
 #pragma unroll
       for (int m = 0; m < MBL; ++m)
@@ -472,7 +474,7 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
     }
   } else {
-    if (a.zsum) {
+    if constexpr (ZSUM) {
       // adjoint over the chunk's planes (see the power-of-two branch)
       float2 acc[FFT_MAXV];
 #pragma unroll
@@ -546,6 +548,18 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
   }
 }
 
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                AsmArgs a) {
+  asm_cols_body<PN, false>(T, U, ph, a);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols_zsum(const float2* __restrict__ T, float2* __restrict__ U,
+                                                     FftPlan ph, AsmArgs a) {
+  asm_cols_body<PN, true>(T, U, ph, a);
+}
+
 // Per (wavelength, band column) of a mixed-radix Ph: sqrt(k^2 - Kx^2 - Ky^2) of every row
 // (z-independent, written on the first z-chunk) and the kept-row bound M_z of each z of the
 // chunk (bisection with the exact reference-order tests, one lane per z; see asm_cols).  Every
@@ -606,9 +620,9 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
 // per-column sqrt and the bisected |m_x| bound, cropped rows stored from the last stage -- with
 // the runtime plan's numerics at the output (1 / (Ph Pw) is not a power of two here, so the
 // scale is applied to each output element as asm_cols<0> does).
-template <class MP>
-__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
-                                                    AsmArgs a) {
+template <class MP, bool ZSUM>
+__device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                 AsmArgs a) {
   constexpr int PN = MP::N, RL = MP::RL, NBL = PN / RL, MBL = (NBL + MX_T - 1) / MX_T;
   static_assert(MP::R0 == RL, "the inverse must start where the forward ends");
   extern __shared__ float2 lds[];
@@ -631,8 +645,8 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
   };
   auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
   const auto twr = MP::template twiddles<MX_T>(ph.tw, tid);
-  if (!a.zsum) MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
-  if (a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
+  if constexpr (!ZSUM) MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
+  if (!ZSUM && a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
     const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
@@ -660,7 +674,7 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
 #pragma unroll
     for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
   }
-  if (a.zsum) {
+  if constexpr (ZSUM) {
     // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
 #pragma unroll
     for (int m = 0; m < MBL; ++m)
@@ -718,6 +732,18 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
     };
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
   }
+}
+
+template <class MP>
+__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx(
+    const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_mx_body<MP, false>(T, U, ph, a);
+}
+
+template <class MP>
+__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_zsum(
+    const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_mx_body<MP, true>(T, U, ph, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1018,6 +1044,7 @@ template <int PN>
 static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_rows_fwd<PN>);
   ks.push_back((const void*)asm_cols<PN>);
+  ks.push_back((const void*)asm_cols_zsum<PN>);
   ks.push_back((const void*)asm_rows_inv<PN>);
   ks.push_back((const void*)asm_rows_inv_loss<PN>);
   ks.push_back((const void*)fft_rows_kernel<PN>);
@@ -1142,10 +1169,10 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
           THZ_LAUNCH_CHECK();
         }
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
-        hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+        hipLaunchKernelGGL(asm_cols_mx_zsum<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-        THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(a.kfull), dim3(th), lds2, s, (const float2*)T, U, ph, a);
+        THZ_POW2_SWITCH(g.Ph, asm_cols_zsum, dim3(a.kfull), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       }
       THZ_LAUNCH_CHECK();
       kt.stop();
