@@ -335,6 +335,57 @@ int thz_resample_backward(const thz_resample_desc* d, const void* grad_out, void
 int thz_fft_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream);
 
 /*
+ * Double precision (complex128).  The reference computes in the field's precision: a complex128
+ * field or float64 wavelength tensor runs ASM / CZT / RSC in fp64 and returns complex128
+ * (DataType/ElectricField.py:85-90; test_czt.py:12 runs RSC + CZT that way).  These entries are
+ * the fp32 ones with double scalars and complex128 buffers (interleaved double (re, im), identical
+ * to torch.complex128); same shapes, windows and error codes.  Transform lengths (padded sizes,
+ * Bluestein np2) up to 8192.  The fp64 ASM adjoint takes one z-plane (Z == 1).
+ */
+typedef struct thz_asm_desc64 {
+  int B, C, H, W;
+  int pad_h, pad_w;
+  int unpad;
+  int bandlimit;             /* THZ_BANDLIMIT_* */
+  int Z;                     /* 1 .. THZ_MAX_Z; 1 for the adjoint */
+  int adjoint;
+  double dx, dy;
+  const double* wavelengths; /* host [C] */
+  const double* z;           /* host [Z] */
+} thz_asm_desc64;
+int thz_asm64_workspace_size(const thz_asm_desc64* d, size_t* bytes);
+int thz_asm64_forward(const thz_asm_desc64* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
+                      thz_stream_t stream);
+
+typedef struct thz_czt_desc64 {
+  int B, C, H, W;
+  int outH, outW;
+  double dx, dy;
+  double odx, ody;
+  double z;
+  const double* wavelengths; /* host [C] */
+  int adjoint;
+} thz_czt_desc64;
+int thz_czt64_workspace_size(const thz_czt_desc64* d, size_t* bytes);
+int thz_czt64_forward(const thz_czt_desc64* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
+                      thz_stream_t stream);
+
+typedef struct thz_rsc_desc64 {
+  int B, C, H, W;
+  int vectorial;
+  double dx, dy;
+  double z;
+  const double* wavelengths; /* host [C] */
+  int adjoint;
+} thz_rsc_desc64;
+int thz_rsc64_workspace_size(const thz_rsc_desc64* d, size_t* bytes);
+int thz_rsc64_forward(const thz_rsc_desc64* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
+                      thz_stream_t stream);
+
+/* Batched 1-D FFT of complex128 rows (as thz_fft_rows), n <= 8192. */
+int thz_fft64_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream);
+
+/*
  * Per-kernel HIP-event timing used by bench.py (not part of the reference): when
  * enabled every kernel launch is bracketed by two events on its own stream;
  * thz_timing_read() synchronises on the pending events and returns the summed

@@ -115,11 +115,13 @@ class _RscFunction(torch.autograd.Function):
         adj = _prop.rsc_apply(g.contiguous(), wavelengths, spacing, z, adjoint=True, field_hw=(H, W))
         if not vectorial:
             return adj, None, None, None, None
-        dx = torch.tensor(spacing[0], dtype=torch.float32)
-        x = torch.linspace(float(-dx * H / 2), float(dx * H / 2), H, device=g.device)
-        y = torch.linspace(float(-dx * W / 2), float(dx * W / 2), W, device=g.device)
+        # the Ez grid in the field's precision (fp32 for complex64, fp64 for complex128)
+        rdt = torch.float64 if adj.dtype == torch.complex128 else torch.float32
+        dx = torch.tensor(spacing[0], dtype=rdt)
+        x = torch.linspace(float(-dx * H / 2), float(dx * H / 2), H, device=g.device, dtype=rdt)
+        y = torch.linspace(float(-dx * W / 2), float(dx * W / 2), W, device=g.device, dtype=rdt)
         X, Y = torch.meshgrid(x, y, indexing="ij")
-        r = torch.sqrt(X ** 2 + Y ** 2 + torch.tensor(z, dtype=torch.float32) ** 2)
+        r = torch.sqrt(X ** 2 + Y ** 2 + torch.tensor(z, dtype=rdt) ** 2)
         gin = torch.zeros(shape, dtype=adj.dtype, device=g.device)
         gin[0] = adj[0] + adj[2] * (X / r)
         gin[1] = adj[1] + adj[2] * (Y / r)

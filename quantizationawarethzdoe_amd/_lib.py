@@ -37,6 +37,8 @@ EXPORTED = [
     "thz_intensity_mse_workspace_size", "thz_intensity_mse_forward", "thz_intensity_mse_backward",
     "thz_resample_forward", "thz_resample_backward",
     "thz_fft_rows",
+    "thz_asm64_workspace_size", "thz_asm64_forward", "thz_czt64_workspace_size", "thz_czt64_forward",
+    "thz_rsc64_workspace_size", "thz_rsc64_forward", "thz_fft64_rows",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
 
@@ -74,6 +76,33 @@ class RscDesc(ctypes.Structure):
         ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
         ("vectorial", ctypes.c_int), ("dx", ctypes.c_float), ("dy", ctypes.c_float), ("z", ctypes.c_float),
         ("wavelengths", ctypes.POINTER(ctypes.c_float)), ("adjoint", ctypes.c_int),
+    ]
+
+
+class AsmDesc64(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("pad_h", ctypes.c_int), ("pad_w", ctypes.c_int),
+        ("unpad", ctypes.c_int), ("bandlimit", ctypes.c_int), ("Z", ctypes.c_int), ("adjoint", ctypes.c_int),
+        ("dx", ctypes.c_double), ("dy", ctypes.c_double),
+        ("wavelengths", ctypes.POINTER(ctypes.c_double)), ("z", ctypes.POINTER(ctypes.c_double)),
+    ]
+
+
+class CztDesc64(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("outH", ctypes.c_int), ("outW", ctypes.c_int),
+        ("dx", ctypes.c_double), ("dy", ctypes.c_double), ("odx", ctypes.c_double), ("ody", ctypes.c_double),
+        ("z", ctypes.c_double), ("wavelengths", ctypes.POINTER(ctypes.c_double)), ("adjoint", ctypes.c_int),
+    ]
+
+
+class RscDesc64(ctypes.Structure):
+    _fields_ = [
+        ("B", ctypes.c_int), ("C", ctypes.c_int), ("H", ctypes.c_int), ("W", ctypes.c_int),
+        ("vectorial", ctypes.c_int), ("dx", ctypes.c_double), ("dy", ctypes.c_double), ("z", ctypes.c_double),
+        ("wavelengths", ctypes.POINTER(ctypes.c_double)), ("adjoint", ctypes.c_int),
     ]
 
 
@@ -182,6 +211,11 @@ def _declare(lib):
                                                c_void_p, c_void_p]
     lib.thz_resample_forward.argtypes = [ctypes.POINTER(ResampleDesc), c_void_p, c_void_p, c_void_p]
     lib.thz_resample_backward.argtypes = [ctypes.POINTER(ResampleDesc), c_void_p, c_void_p, c_void_p]
+    for tag, desc in (("asm64", AsmDesc64), ("czt64", CztDesc64), ("rsc64", RscDesc64)):
+        getattr(lib, f"thz_{tag}_workspace_size").argtypes = [ctypes.POINTER(desc), ctypes.POINTER(c_size_t)]
+        getattr(lib, f"thz_{tag}_forward").argtypes = [ctypes.POINTER(desc), c_void_p, c_void_p, c_void_p, c_size_t,
+                                                       c_void_p]
+    lib.thz_fft64_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]
     lib.thz_timing_reset.argtypes = []
     lib.thz_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]
@@ -231,6 +265,10 @@ def timing_read(kernel):
     ms, n = ctypes.c_double(0), ctypes.c_long(0)
     check(lib().thz_timing_read(kernel.encode(), ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+def double_array(values):
+    return (ctypes.c_double * max(1, len(values)))(*[float(v) for v in values])
 
 
 def float_array(values):

@@ -79,6 +79,11 @@ def modulate_backward(g, field, height, noise, tol, eps, tand, wavelengths, need
 def _modulate_args(field, height, tolerance, noise, rng=None):
     from quantizationawarethzdoe_amd.propagation import kernel_dtype
     field = kernel_dtype(field, "DOE modulate")
+    if field.dtype == torch.complex128:
+        # the propagators have fp64 kernels (csrc/thz_f64.hip); the DOE layers compute in complex64
+        raise TypeError("DOE modulate: the DOE kernels compute in complex64; got a complex128 field (the "
+                        "reference would compute it in fp64, DataType/ElectricField.py:85-90) -- cast the field "
+                        "to complex64 before the DOE layer")
     if tolerance is not None and noise is None and rng is None:
         noise = torch.rand_like(height)
     if noise is not None:

@@ -25,23 +25,18 @@ def _require_device(t: torch.Tensor, what: str):
 
 
 def kernel_dtype(data: torch.Tensor, who: str, wavelengths=None) -> torch.Tensor:
-    """The field as the kernels' complex64.  The reference computes in the field's own precision: a
-    float64 wavelength tensor or complex128 data runs it in fp64 and returns complex128
-    (DataType/ElectricField.py:85-90; its smoke script test_czt.py:12 does so).  The MI355X kernels
-    are fp32 only, and narrowing a complex128 field without a word would hand back fp32 accuracy
-    under an fp64 dtype, so double precision is refused with TypeError (as the DOE modulation
-    does); real float32 data is promoted to complex64 as torch's complex products promote it."""
-    if torch.is_tensor(wavelengths) and wavelengths.dtype == torch.float64:
-        raise TypeError(f"{who}: float64 wavelengths make the reference compute in fp64 and return complex128 "
-                        f"(DataType/ElectricField.py:85-90); the MI355X kernels compute in fp32 -- pass float32 "
-                        f"wavelengths (a float / list, or a float32 tensor).")
-    if data.dtype == torch.complex64:
-        return data
-    if data.dtype in (torch.float32, torch.float16, torch.bfloat16):
-        return data.to(torch.complex64)
-    raise TypeError(f"{who}: the MI355X kernels compute in complex64 (fp32); got {data.dtype}. The reference "
-                    f"runs double-precision fields in fp64 (DataType/ElectricField.py:85-90); this build does not "
-                    f"-- cast the field to complex64 (e.g. ElectricField(data.to(torch.complex64), ...)).")
+    """The field in the precision the reference computes it in (DataType/ElectricField.py:85-90):
+    complex128 when the data is complex128 / float64 or the wavelength tensor is float64 (torch's
+    promotion; the reference's test_czt.py:12 runs that way), else complex64.  The complex128
+    fields run the fp64 kernels (csrc/thz_f64.hip), the rest the fp32 ones; real data is promoted
+    as torch's complex products promote it."""
+    fp64 = data.dtype in (torch.complex128, torch.float64) or (
+        torch.is_tensor(wavelengths) and wavelengths.dtype == torch.float64)
+    if data.dtype not in (torch.complex64, torch.complex128, torch.float32, torch.float64, torch.float16,
+                          torch.bfloat16):
+        raise TypeError(f"{who}: the MI355X kernels compute in complex64 or complex128; got {data.dtype}")
+    want = torch.complex128 if fp64 else torch.complex64
+    return data if data.dtype == want else data.to(want)
 
 
 def _stream_handle():
@@ -74,8 +69,10 @@ def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, ad
     over the Z planes of each plane's adjoint (one pipeline: the column pass sums the planes'
     spectra, thz_asm_forward with adjoint = 1)."""
     _require_device(data, "ASM")
+    if data.dtype == torch.complex128:
+        return _asm64_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint, out)
     if data.dtype != torch.complex64:
-        raise TypeError(f"ASM kernels compute in complex64; got {data.dtype}")
+        raise TypeError(f"ASM kernels compute in complex64 or complex128; got {data.dtype}")
     L = _lib.lib()
     data = data.contiguous()
     if adjoint:
@@ -99,6 +96,49 @@ def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, ad
         _lib.check(L.thz_asm_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
                                      ctypes.c_size_t(ws.numel()), _stream_handle()))
+    return out
+
+
+def _asm64_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint=False, out=None):
+    """complex128 ASM (thz_asm64_forward): the same shapes as asm_apply; the fp64 adjoint runs one
+    launch per plane and sums them."""
+    L = _lib.lib()
+    data = data.contiguous()
+    if adjoint:
+        Z, B, C, Ho, Wo = data.shape
+        if Z != len(zs):
+            raise ValueError(f"adjoint: {Z} gradient planes for {len(zs)} z values")
+        H = Ho - (0 if unpad else 2 * pad_h)
+        W = Wo - (0 if unpad else 2 * pad_w)
+        res = None
+        for k, z in enumerate(zs):
+            gk = _asm64_launch(data[k:k + 1], (B, C, H, W), wavelengths, spacing, [z], pad_h, pad_w, unpad, bandlimit,
+                               True, torch.empty((B, C, H, W), dtype=torch.complex128, device=data.device))
+            res = gk if res is None else res + gk
+        return res
+    B, C, H, W = data.shape
+    Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
+    if out is None:
+        out = torch.empty((len(zs), B, C, Ho, Wo), dtype=torch.complex128, device=data.device)
+    return _asm64_launch(data, (B, C, H, W), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, False, out)
+
+
+def _asm64_launch(data, shape, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint, out):
+    L = _lib.lib()
+    B, C, H, W = shape
+    wl = _lib.double_array(wavelengths)
+    zv = _lib.double_array(zs)
+    d = _lib.AsmDesc64(B=B, C=C, H=H, W=W, pad_h=pad_h, pad_w=pad_w, unpad=int(bool(unpad)), bandlimit=int(bandlimit),
+                       Z=len(zs), adjoint=int(adjoint), dx=float(spacing[0]), dy=float(spacing[1]),
+                       wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_double)),
+                       z=ctypes.cast(zv, ctypes.POINTER(ctypes.c_double)))
+    nbytes = ctypes.c_size_t(0)
+    _lib.check(L.thz_asm64_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+    ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
+    with torch.cuda.device(data.device):
+        _lib.check(L.thz_asm64_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
+                                       ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                                       ctypes.c_size_t(ws.numel()), _stream_handle()))
     return out
 
 
@@ -317,15 +357,18 @@ def deferring():
 
 
 def fft_rows(x, inverse=False):
-    """Unnormalised batched 1-D FFT along the last axis with the LDS Stockham kernel."""
+    """Unnormalised batched 1-D FFT along the last axis with the LDS Stockham kernel (complex128
+    input: the fp64 transform)."""
     _require_device(x, "fft_rows")
-    x = x.contiguous().to(torch.complex64)
+    x = x.contiguous()
+    x = x if x.dtype == torch.complex128 else x.to(torch.complex64)
     out = torch.empty_like(x)
     n = x.shape[-1]
     rows = x.numel() // n
+    fn = _lib.lib().thz_fft64_rows if x.dtype == torch.complex128 else _lib.lib().thz_fft_rows
     with torch.cuda.device(x.device):
-        _lib.check(_lib.lib().thz_fft_rows(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()),
-                                           rows, n, int(inverse), _stream_handle()))
+        _lib.check(fn(ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(out.data_ptr()), rows, n, int(inverse),
+                      _stream_handle()))
     return out
 
 
@@ -334,27 +377,35 @@ def czt_apply(data, wavelengths, spacing, z, outH, outW, odx, ody, adjoint=False
 
     adjoint: the autograd backward, [B,C,outW,outH] -> [B,C,H,W] with (H, W) = field_hw."""
     _require_device(data, "CZT")
-    if data.dtype != torch.complex64:
-        raise TypeError(f"CZT kernels compute in complex64; got {data.dtype}")
+    if data.dtype not in (torch.complex64, torch.complex128):
+        raise TypeError(f"CZT kernels compute in complex64 or complex128; got {data.dtype}")
+    f64 = data.dtype == torch.complex128
     data = data.contiguous()
     B, C = data.shape[:2]
     H, W = (int(v) for v in (field_hw if adjoint else data.shape[-2:]))
     if adjoint and tuple(data.shape[-2:]) != (int(outW), int(outH)):
         raise ValueError(f"CZT adjoint: gradient {tuple(data.shape)} is not [B, C, outW, outH]")
-    wl = _lib.float_array(wavelengths)
-    d = _lib.CztDesc(B=B, C=C, H=H, W=W, outH=int(outH), outW=int(outW), dx=float(spacing[0]),
-                     dy=float(spacing[1]), odx=float(odx), ody=float(ody), z=float(z),
-                     wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)), adjoint=int(bool(adjoint)))
+    if f64:
+        wl = _lib.double_array(wavelengths)
+        d = _lib.CztDesc64(B=B, C=C, H=H, W=W, outH=int(outH), outW=int(outW), dx=float(spacing[0]),
+                           dy=float(spacing[1]), odx=float(odx), ody=float(ody), z=float(z),
+                           wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_double)), adjoint=int(bool(adjoint)))
+    else:
+        wl = _lib.float_array(wavelengths)
+        d = _lib.CztDesc(B=B, C=C, H=H, W=W, outH=int(outH), outW=int(outW), dx=float(spacing[0]),
+                         dy=float(spacing[1]), odx=float(odx), ody=float(ody), z=float(z),
+                         wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)), adjoint=int(bool(adjoint)))
     L = _lib.lib()
+    size_fn, run_fn = (L.thz_czt64_workspace_size, L.thz_czt64_forward) if f64 else \
+        (L.thz_czt_workspace_size, L.thz_czt_forward)
     nbytes = ctypes.c_size_t(0)
-    _lib.check(L.thz_czt_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+    _lib.check(size_fn(ctypes.byref(d), ctypes.byref(nbytes)))
     ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
     oshape = (B, C, H, W) if adjoint else (B, C, int(outW), int(outH))
-    out = torch.empty(oshape, dtype=torch.complex64, device=data.device)
+    out = torch.empty(oshape, dtype=data.dtype, device=data.device)
     with torch.cuda.device(data.device):
-        _lib.check(L.thz_czt_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
-                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                                     ctypes.c_size_t(ws.numel()), _stream_handle()))
+        _lib.check(run_fn(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                          ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()), _stream_handle()))
     return out
 
 
@@ -366,28 +417,36 @@ def rsc_apply(data, wavelengths, spacing, z, vectorial=False, adjoint=False, fie
     (H, W) = field_hw, the forward field's shape.
     """
     _require_device(data, "RSC")
-    if data.dtype != torch.complex64:
-        raise TypeError(f"RSC kernels compute in complex64; got {data.dtype}")
+    if data.dtype not in (torch.complex64, torch.complex128):
+        raise TypeError(f"RSC kernels compute in complex64 or complex128; got {data.dtype}")
+    f64 = data.dtype == torch.complex128
     data = data.contiguous()
     B, C = data.shape[:2]
     H, W = field_hw if adjoint else data.shape[-2:]
-    wl = _lib.float_array(wavelengths)
-    d = _lib.RscDesc(B=B, C=C, H=int(H), W=int(W), vectorial=int(bool(vectorial)), dx=float(spacing[0]),
-                     dy=float(spacing[1]), z=float(z), wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
-                     adjoint=int(bool(adjoint)))
+    if f64:
+        wl = _lib.double_array(wavelengths)
+        d = _lib.RscDesc64(B=B, C=C, H=int(H), W=int(W), vectorial=int(bool(vectorial)), dx=float(spacing[0]),
+                           dy=float(spacing[1]), z=float(z),
+                           wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_double)), adjoint=int(bool(adjoint)))
+    else:
+        wl = _lib.float_array(wavelengths)
+        d = _lib.RscDesc(B=B, C=C, H=int(H), W=int(W), vectorial=int(bool(vectorial)), dx=float(spacing[0]),
+                         dy=float(spacing[1]), z=float(z), wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
+                         adjoint=int(bool(adjoint)))
     L = _lib.lib()
+    size_fn, run_fn = (L.thz_rsc64_workspace_size, L.thz_rsc64_forward) if f64 else \
+        (L.thz_rsc_workspace_size, L.thz_rsc_forward)
     nbytes = ctypes.c_size_t(0)
-    _lib.check(L.thz_rsc_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
+    _lib.check(size_fn(ctypes.byref(d), ctypes.byref(nbytes)))
     ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
     if adjoint:
         if tuple(data.shape[-2:]) != (2 * (H // 2), 2 * (W // 2)):
             raise ValueError(f"RSC adjoint: gradient {tuple(data.shape)} does not match field {(H, W)}")
-        out = torch.empty((B, C, int(H), int(W)), dtype=torch.complex64, device=data.device)
+        out = torch.empty((B, C, int(H), int(W)), dtype=data.dtype, device=data.device)
     else:
         Bo = 3 if vectorial else B
-        out = torch.empty((Bo, C, 2 * (H // 2), 2 * (W // 2)), dtype=torch.complex64, device=data.device)
+        out = torch.empty((Bo, C, 2 * (H // 2), 2 * (W // 2)), dtype=data.dtype, device=data.device)
     with torch.cuda.device(data.device):
-        _lib.check(L.thz_rsc_forward(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()),
-                                     ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                                     ctypes.c_size_t(ws.numel()), _stream_handle()))
+        _lib.check(run_fn(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(out.data_ptr()),
+                          ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()), _stream_handle()))
     return out

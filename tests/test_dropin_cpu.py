@@ -90,28 +90,31 @@ def test_doe_save_writes_the_reference_bytes(tmp_path, monkeypatch):
     assert d["thickness"].shape == tuple(c["crop"]) and float(d["dxy"]) == c["doe_params"]["doe_dxy"]
 
 
-@pytest.mark.parametrize("which", ["asm", "czt", "rsc"])
-def test_double_precision_is_refused(which):
-    """The reference computes a complex128 field (or float64 wavelengths) in fp64 and returns
-    complex128 (DataType/ElectricField.py:85-90); the fp32 kernels refuse it with TypeError
-    rather than narrow it silently (as doe.modulate does)."""
+def test_compute_dtype_follows_the_reference_promotion():
+    """The reference computes in the field's precision (DataType/ElectricField.py:85-90): a complex128
+    field or a float64 wavelength tensor runs in fp64 and returns complex128, real float32 data
+    promotes to complex64.  kernel_dtype picks the kernels' precision the same way; the DOE
+    layers (complex64 kernels only) refuse complex128 with TypeError, and a CPU tensor still
+    raises before any work (there is no CPU compute path)."""
     from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
     from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
-    from quantizationawarethzdoe_amd.Props.CZT_Prop import CZT_prop
-    from quantizationawarethzdoe_amd.Props.RSC_Prop import RSC_prop
-    prop = {"asm": lambda: ASM_prop(z_distance=0.1, device="cpu"), "czt": lambda: CZT_prop(z_distance=0.1, device="cpu"),
-            "rsc": lambda: RSC_prop(z_distance=0.5, device="cpu")}[which]()
+    from quantizationawarethzdoe_amd import doe
+    from quantizationawarethzdoe_amd.propagation import kernel_dtype
+    c64, c128 = torch.zeros(1, 1, 4, 4, dtype=torch.complex64), torch.zeros(1, 1, 4, 4, dtype=torch.complex128)
+    assert kernel_dtype(c64, "t").dtype == torch.complex64
+    assert kernel_dtype(c128, "t").dtype == torch.complex128
+    assert kernel_dtype(torch.zeros(1, 1, 4, 4), "t").dtype == torch.complex64
+    assert kernel_dtype(torch.zeros(1, 1, 4, 4, dtype=torch.float64), "t").dtype == torch.complex128
+    assert kernel_dtype(c64, "t", torch.tensor([1e-3], dtype=torch.float64)).dtype == torch.complex128
+    assert kernel_dtype(c64, "t", torch.tensor([1e-3], dtype=torch.float32)).dtype == torch.complex64
+    with pytest.raises(TypeError):
+        kernel_dtype(torch.zeros(2, dtype=torch.int32), "t")
+    with pytest.raises(TypeError, match="complex64"):
+        doe.modulate(c128, torch.zeros(4, 4), [1e-3], 2.66, 0.03)
     cpu = torch.device("cpu")
     f128 = ElectricField(torch.ones(1, 1, 16, 16, dtype=torch.complex128), wavelengths=1e-3, spacing=1e-3, device=cpu)
-    with pytest.raises(TypeError, match="complex64"):
-        prop(f128)
-    f64wl = ElectricField(torch.ones(1, 1, 16, 16, dtype=torch.complex64),
-                          wavelengths=torch.tensor([1e-3], dtype=torch.float64), spacing=1e-3, device=cpu)
-    with pytest.raises(TypeError, match="float64 wavelengths"):
-        prop(f64wl)
-    f32 = ElectricField(torch.ones(1, 1, 16, 16, dtype=torch.complex64), wavelengths=1e-3, spacing=1e-3, device=cpu)
     with pytest.raises(RuntimeError, match="ROCm device"):
-        prop(f32)
+        ASM_prop(z_distance=0.1, device="cpu")(f128)
 
 
 def test_doe_xyz_coordinates_export(tmp_path, monkeypatch, capsys):
