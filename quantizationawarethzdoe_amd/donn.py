@@ -227,6 +227,13 @@ class DONNTrainer:
                         if torch.is_tensor(v):
                             v.copy_(saved[k]) if saved is not None else v.zero_()
             self.optimizer.zero_grad(set_to_none=True)
+            if self.allreduce.world == 1:
+                # no collective: the whole step (fwd/bwd, Adam) is one graph, one replay per step
+                g_fb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_fb):
+                    loss = self._fb(su, st, frac)
+                    self._opt()
+                return g_fb, None, loss
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb):
                 loss = self._fb(su, st, frac)
@@ -248,8 +255,9 @@ class DONNTrainer:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
         g_fb.replay()
-        self.allreduce.reduce()
-        g_opt.replay()
+        if g_opt is not None:  # world > 1: the collective between the two captured halves
+            self.allreduce.reduce()
+            g_opt.replay()
         return loss
 
 

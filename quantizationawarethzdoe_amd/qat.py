@@ -227,8 +227,9 @@ class QATTrainer:
     overhead.  The schedule values that change every step (tau, s = tau_max / tau, beta) reach
     the quantizer kernels through a 3-float device buffer (thz_quant_desc.dyn), and the
     Gumbel / height-noise draws are graph-safe philox draws, so each replay is a fresh sample.
-    With N ranks the replay is split around the (eager) gradient all-reduce.  The random
-    stream differs from the eager path (same distribution, different draws).
+    On one rank the whole step (forward, loss, backward, Adam) is ONE graph; with N ranks the
+    replay is split around the (eager) gradient all-reduce.  The random stream differs from the
+    eager path (same distribution, different draws).
     """
 
     def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False, loss_fn=None,
@@ -317,6 +318,13 @@ class QATTrainer:
                         if torch.is_tensor(v):
                             v.copy_(saved[k]) if saved is not None else v.zero_()
             self.optimizer.zero_grad(set_to_none=True)
+            if self.allreduce.world == 1:
+                # no collective: the whole step (fwd/bwd, Adam) is one graph, one replay per step
+                g_fb = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g_fb):
+                    loss = self._fb(frac)
+                    self._opt()
+                return g_fb, None, loss
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb):
                 loss = self._fb(frac)
@@ -331,8 +339,9 @@ class QATTrainer:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
         g_fb.replay()
-        self.allreduce.reduce()
-        g_opt.replay()
+        if g_opt is not None:  # world > 1: the collective between the two captured halves
+            self.allreduce.reduce()
+            g_opt.replay()
         return loss
 
     def train(self, steps, log_every=200, log=print):

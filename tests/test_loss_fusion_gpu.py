@@ -155,3 +155,50 @@ def test_donn_default_loss_fused_matches():
     assert np.allclose(la, lb, rtol=2e-5, atol=0)
     for a, b in zip(pa, pb):
         assert rel_l2(a.numpy(), b.numpy()) <= 1e-4
+
+
+@pytest.mark.parametrize("fused", [False, True], ids=["separate", "fused"])
+def test_loss_near_convergence_vs_fp64_oracle(fused):
+    """A near-converged field (normalised intensity = target up to ~1e-4): the loss kernels form
+    sum (I/m - T)^2 as S_II/m^2 - 2 S_IT/m + S_TT from one-pass fp64 sums (ADVICE round 2 asked
+    whether that cancels catastrophically).  In fp64 the cancellation costs ~1e-16 S_TT / loss
+    ~ 1e-9 relative here; what remains is the fp32 rounding of |E|^2 itself (~6e-8 of I against
+    residuals of ~1e-4), so the bound vs the fp64 oracle of the same fp32 field is 1e-2 relative
+    -- a cancelling fp32 form would be off by O(1).  The loss is ~1e-8 against S_TT / n ~ 0.3.
+    Gradient (2 E dL/dI): rel-L2 <= 1e-2 on the same grounds."""
+    from quantizationawarethzdoe_amd import optics, propagation as P
+    dev = _dev()
+    g = torch.Generator().manual_seed(8)
+    shape = (2, 1, 100, 100)
+    x = (torch.randn(shape, generator=g) + 1j * torch.randn(shape, generator=g)).to(torch.complex64)
+    wl, sp, z = _wl(1), (1e-3, 1e-3), 0.12
+    ph, pw = P.asm_padding(100, 100, (2, 2))
+    with torch.no_grad():
+        E = P.asm_propagate(x.to(dev), wl, sp, [z], ph, pw)[0]
+        I = E.abs().double() ** 2
+        I = I / I.amax(dim=(1, 2, 3), keepdim=True)
+        tgt = (I * (1 + 1e-4 * torch.randn(I.shape, generator=g).to(dev).double())).float()
+    xd = x.to(dev).requires_grad_(True)
+    if fused:
+        # the loss of the field the fused pipeline stored, in fp64 (isolates the loss arithmetic from
+        # the fp32 propagation); the gradient vs the separate path's through the same kernels
+        out, loss = P.asm_propagate_loss(xd, tgt, wl, sp, z, ph, pw)
+        loss.backward()
+        gx = xd.grad
+        ref = orc.intensity_mse(out.detach().cpu().to(torch.complex128), tgt.cpu().double())
+        xs = x.to(dev).requires_grad_(True)
+        optics.intensity_mse(P.asm_propagate(xs, wl, sp, [z], ph, pw)[0], tgt).backward()
+        rg = xs.grad.cpu()
+    else:
+        Ed = E.clone().requires_grad_(True)
+        loss = optics.intensity_mse(Ed, tgt)
+        loss.backward()
+        gx = Ed.grad
+        Eo = E.cpu().to(torch.complex128).requires_grad_(True)
+        ref = orc.intensity_mse(Eo, tgt.cpu().double())
+        ref.backward()
+        rg = Eo.grad
+    lv, rv = float(loss.detach()), float(ref.detach())
+    assert 1e-10 < rv < 1e-6, rv  # near convergence: the loss is ~1e-8 of the target's scale
+    assert abs(lv - rv) <= 1e-2 * rv, (lv, rv)
+    assert rel_l2(gx.cpu().numpy(), rg.numpy()) <= 1e-2
