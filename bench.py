@@ -684,8 +684,9 @@ def main():
     for key, sec in (line.get("secondary") or {}).items():
         if sec is None:
             continue
-        if "error" in sec:
-            failed.append(f"{key}: {sec['error']}")
+        if "error" in sec:  # reported in the line; only a wrong result fails the run
+            sys.stderr.write(f"bench.py: {key} did not run: {sec['error']}\n")
+            continue
         parts = [sec] if "output_check" in sec else list((sec.get("modes") or {}).values())
         for part in parts:
             chk = part.get("output_check")

@@ -185,7 +185,7 @@ def test_loss_near_convergence_vs_fp64_oracle(fused):
         out, loss = P.asm_propagate_loss(xd, tgt, wl, sp, z, ph, pw)
         loss.backward()
         gx = xd.grad
-        ref = orc.intensity_mse(out.detach().cpu().to(torch.complex128), tgt.cpu().double())
+        ref = orc.intensity_mse(out[0].detach().cpu().to(torch.complex128), tgt.cpu().double())
         xs = x.to(dev).requires_grad_(True)
         optics.intensity_mse(P.asm_propagate(xs, wl, sp, [z], ph, pw)[0], tgt).backward()
         rg = xs.grad.cpu()
