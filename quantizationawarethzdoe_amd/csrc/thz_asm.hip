@@ -23,7 +23,8 @@
 #include <map>
 #include <mutex>
 #include <cmath>
-#include <mutex>
+#include <cstdlib>
+#include <tuple>
 #include <vector>
 
 #include "thz_common.hpp"
@@ -302,11 +303,22 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
 // ---------------------------------------------------------------------------------------------
 // ZSUM: the Z-summing adjoint's column pass (a separate instantiation, so the forward's register
-// allocation is untouched by it)
-template <int PN, bool ZSUM>
+// allocation is untouched by it).
+// NCOL = 2 (power-of-two PN <= 8192): one workgroup transforms the adjacent band columns 2p and
+// 2p + 1 in lockstep, each half on its own LDS image, sharing the twiddle tables.  The U sectors
+// (CBU = 4 columns) then have two writers instead of four, and the pair's stores to a sector are
+// issued together.
+template <int PN, int NCOL>
+__device__ __forceinline__ int col_tid() {
+  if constexpr (NCOL == 2) return (int)threadIdx.x & (Geo<PN>::T - 1);
+  else return (int)threadIdx.x;
+}
+
+template <int PN, bool ZSUM, int NCOL = 1>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
-  extern __shared__ float2 lds[];
+  static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
+  extern __shared__ float2 lds0[];
   // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
   // resident-workgroup count), the last partial round's columns are split into kparts z-ranges
   // so that round is short instead of a whole column pass on a few CUs.
@@ -319,8 +331,13 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     z_lo = part * a.nz / a.kparts;
     z_hi = (part + 1) * a.nz / a.kparts;
   }
-  const int bc = id / a.ncols, c = id - bc * a.ncols;
-  const int nt = blockDim.x;
+  const int ntask = NCOL == 1 ? a.ncols : (a.ncols + 1) / 2;  // column tasks per (b, c) plane
+  const int bc = id / ntask, half = NCOL == 1 ? 0 : (int)threadIdx.x / (int)(blockDim.x / NCOL);
+  int c = (id - bc * ntask) * NCOL + half;
+  const bool live = c < a.ncols;  // the odd last column's partner half runs without storing
+  if (!live) c = a.ncols - 1;
+  const int nt = blockDim.x / NCOL;
+  float2* const lds = lds0 + (PN > 0 ? half * lds_floats2(PN) : 0);
   const int Ph = a.Ph;
   const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
   const float lam = a.lam[bc % a.C];
@@ -328,7 +345,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
   // Each phase works from its own opaque copy of threadIdx.x: otherwise the compiler CSEs /
   // hoists the forward and inverse transforms' LDS addresses and twiddle loads across the
   // whole kernel and spills (the two transforms share every twiddle address).
-  int tid = threadIdx.x;
+  int tid = col_tid<PN, NCOL>();
   if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = Geo<PN>::T;
@@ -338,7 +355,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     constexpr int RL = S::radix(S::NST - 1, true);   // radix of the forward's last stage
     constexpr int MBL = PN / RL / TT;                // its butterflies per thread
     float2 sp[MBL][RL];                              // spectrum, element i + r*PN/RL
-    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), ph.tw, tid, nt);
+    const TwLds twl = load_tw_lds<PN>(lds0 + NCOL * lds_floats2(PN), ph.tw, threadIdx.x, blockDim.x);
     auto ld0 = [&](int, int, int idx) {
       const int s = idx - a.in_r0;
       return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
@@ -355,7 +372,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     }
     if (!ZSUM && a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
-      int tz = threadIdx.x;
+      int tz = col_tid<PN, NCOL>();
       asm volatile("" : "+v"(tz));
       auto ld1 = [&](int m, int r, int idx) {
         const float2 t = tcol[idx];
@@ -364,7 +381,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+        if (live && r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
       };
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
       return;
@@ -374,12 +391,12 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     // exactly |m_x| <= M_z.  One lane per z finds M_z by bisection with the exact
     // reference-order tests; the per-element work is then sqrt once per column and one
     // sincos per z.
-    int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN) + tw_lds_count(PN));
+    int* mz = reinterpret_cast<int*>(lds0 + NCOL * lds_floats2(PN) + tw_lds_count(PN)) + half * THZ_MAX_Z;
     const float kl = TWO_PI_F / lam;
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
     // strided over the chunk: a z_chunk may exceed the workgroup (64 threads at P = 1024)
-    for (int zz = threadIdx.x; zz < z_hi - z_lo; zz += nt) {
+    for (int zz = tid; zz < z_hi - z_lo; zz += nt) {
       const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + zz]);
       int lo = -1, hi = PN / 2 + 1;
       const int bl = a.bl, P = a.Ph;
@@ -448,7 +465,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     for (int zz = z_lo; zz < z_hi; ++zz) {
       const float z = a.zv[a.zoff + zz];
       const int M = mz[zz - z_lo];
-      int tz = threadIdx.x;
+      int tz = col_tid<PN, NCOL>();
       asm volatile("" : "+v"(tz));
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
@@ -469,7 +486,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         const int r = j - a.out_r0;
         // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2;
         // streaming stores here ran K2 4.1 -> 13.8 ms)
-        if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v;
+        if (live && (unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v;
       };
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
     }
@@ -552,6 +569,12 @@ template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   asm_cols_body<PN, false>(T, U, ph, a);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols_pair(const float2* __restrict__ T, float2* __restrict__ U,
+                                                     FftPlan ph, AsmArgs a) {
+  asm_cols_body<PN, false, 2>(T, U, ph, a);
 }
 
 template <int PN>
@@ -1069,6 +1092,10 @@ static int ensure_lds_attr() {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       if (e != hipSuccess) err = e;
     }
+    const int mxp = (int)(2 * lds_floats2(8192) + tw_lds_count(8192)) * (int)sizeof(float2) + 2 * 4 * THZ_MAX_Z;
+    const hipError_t e = hipFuncSetAttribute((const void*)asm_cols_pair<8192>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, mxp);
+    if (e != hipSuccess) err = e;
   });
   if (err != hipSuccess) return fail(THZ_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s",
                                      hipGetErrorString(err));
@@ -1085,13 +1112,29 @@ static int mx_kind(int n) { return is_mx(n) ? n : 0; }
   if (mx_kind(n) == Mx300::N) hipLaunchKernelGGL(KER<Mx300::N>, G, dim3(MX_T), LDSB, __VA_ARGS__); \
   else THZ_POW2_SWITCH(n, KER, G, dim3(threads_for(n)), LDSB, __VA_ARGS__)
 
-static int k2_resident(int Ph, int threads, size_t lds) {
+// Paired-column K2 (asm_cols_pair) at Ph = 8192, opt-in with THZ_K2_PAIR=1: 2 x 512 threads, two
+// 70 KB LDS images, 127 VGPRs without spills (the 2048 / 4096 pairs spill a few).  Measured on
+// cfg2 (profiles/r03_k2_pair_experiment.txt): its U writes are exactly U (WRITE_SIZE 8.62 GB per
+// launch against 14.47 GB for the one-column kernel), but one 16-wave workgroup per CU stalls at
+// every barrier where two 8-wave workgroups overlap theirs: 4.39 ms against 4.16 ms.  The pass is
+// issue-bound, not write-bound, so the one-column kernel stays the default.
+static bool k2_pair(int Ph) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K2_PAIR");
+    return e && e[0] == '1';
+  }();
+  return on && Ph == 8192;
+}
+static size_t k2_pair_lds(int Ph) {
+  return (size_t)(2 * lds_floats2(Ph) + tw_lds_count(Ph)) * sizeof(float2) + 2 * 4 * THZ_MAX_Z;
+}
+static int k2_resident(int Ph, bool pair, int threads, size_t lds) {
   static std::mutex mu;
-  static std::map<std::pair<int, int>, int> cache;
+  static std::map<std::tuple<int, int, bool>, int> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_pair(dev, Ph);
+  auto key = std::make_tuple(dev, Ph, pair);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const void* k = nullptr;
@@ -1099,7 +1142,7 @@ static int k2_resident(int Ph, int threads, size_t lds) {
     case 1024: k = (const void*)asm_cols<1024>; break;
     case 2048: k = (const void*)asm_cols<2048>; break;
     case 4096: k = (const void*)asm_cols<4096>; break;
-    case 8192: k = (const void*)asm_cols<8192>; break;
+    case 8192: k = pair ? (const void*)asm_cols_pair<8192> : (const void*)asm_cols<8192>; break;
     case 16384: k = (const void*)asm_cols<16384>; break;
     default: k = (const void*)asm_cols<0>; break;
   }
@@ -1114,9 +1157,9 @@ static int k2_resident(int Ph, int threads, size_t lds) {
 }
 
 // K2 task split: whole columns for the full dispatch rounds, the remainder split by z-range.
-static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds) {
-  const int nc = g.ncols * g.BC;
-  const int G = k2_resident(g.Ph, threads, lds);
+static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds, bool pair = false) {
+  const int nc = (pair ? (g.ncols + 1) / 2 : g.ncols) * g.BC;
+  const int G = k2_resident(g.Ph, pair, threads, lds);
   if (G <= 0 || a->nz <= 1) {
     a->kfull = nc;
     a->kparts = 1;
@@ -1229,6 +1272,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+      } else if (k2_pair(g.Ph)) {
+        const size_t lds2 = k2_pair_lds(g.Ph);
+        const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);
+        hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2);

@@ -219,6 +219,39 @@ def test_asm_cfg2_default_chunk_vs_oracle():
             assert e <= 1e-4, (k, zs[k], e)
 
 
+_PAIR_SCRIPT = r"""
+import hashlib, sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_asm_gpu import _cfg2_input
+from quantizationawarethzdoe_amd.propagation import asm_apply
+x, lam = _cfg2_input(torch.device("cuda:0"))
+sp = [float(torch.tensor(0.25e-3, dtype=torch.float32))] * 2
+zs = [float(v) for v in torch.linspace(20e-3, 120e-3, 6, dtype=torch.float64)]
+out = asm_apply(x, [lam], sp, zs, 2048, 2048, True, 1)
+print(hashlib.sha256(out.cpu().numpy().tobytes()).hexdigest())
+"""
+
+
+def test_asm_paired_column_kernel_bit_identical():
+    """The opt-in paired-column K2 (THZ_K2_PAIR=1, asm_cols_pair<8192>: two band columns per
+    workgroup, the odd last column's partner half computing without storing, the z-range split of
+    the last dispatch round) gives bit-identical planes to the default one-column kernel on the
+    cfg2 geometry (same arithmetic per column; 6 planes, sha256 of the output)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = _PAIR_SCRIPT.format(root=root)
+    digests = []
+    for flag in ("1", "0"):
+        env = dict(os.environ, THZ_K2_PAIR=flag)
+        r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
+                           timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        digests.append(r.stdout.strip().splitlines()[-1])
+    assert digests[0] == digests[1]
+
+
 def test_asm_p2048_64_planes_every_plane_vs_oracle():
     """asm_cols<2048> over 64 planes in two full 32-plane chunks (the kparts split of each chunk's
     last dispatch round included): every plane vs the fp64 oracle, <= max(1e-4, 1.5 x the oracle's
