@@ -108,6 +108,8 @@ int thz_asm_band(const thz_asm_desc* d, int* ncols, int* z_chunk);
  *        as the reference's final F0 * U broadcast requires, :248)
  * wavelengths[C] host floats; z, output spacing (odx, ody) as in forward(field, outputHeight,
  * outputWidth, outputPixel_dx, outputPixel_dy).
+ * THZ_E_ARG when H + outW - 1 or W + outH - 1 is a power of two: the reference's Bluestein
+ * slice keeps one row too few there and raises (Props/CZT_Prop.py:206,211).
  */
 typedef struct thz_czt_desc {
   int B, C, H, W;

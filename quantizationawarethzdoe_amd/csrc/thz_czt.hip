@@ -576,6 +576,14 @@ static int czt_validate(const thz_czt_desc* d) {
   if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
   if (!d->wavelengths) return fail(THZ_E_ARG, "null wavelengths");
   const int nA = np2_of(d->W + d->outH - 1), nB = np2_of(d->H + d->outW - 1);
+  // mp = m + M - 1 a power of two: the reference's np2 = 2^ceil(log2 mp) equals mp, its slice
+  // b[m:mp+1] of the np2 inverse then has M - 1 rows and the product with the M-entry chirp
+  // h[m-1:mp] raises (Props/CZT_Prop.py:206,211).  Refused here instead of leaving row M - 1 unset.
+  if (nA == d->W + d->outH - 1 || nB == d->H + d->outW - 1)
+    return fail(THZ_E_ARG, "CZT Bluestein length m + M - 1 = %d is a power of two: the reference's slice "
+                           "b[m:mp+1] keeps M - 1 rows there and its product with h[m-1:mp] raises "
+                           "(Props/CZT_Prop.py:206,211)",
+                nA == d->W + d->outH - 1 ? nA : nB);
   if (nA > FFT_MAX_N || nB > FFT_MAX_N)
     return fail(THZ_E_UNSUPPORTED, "Bluestein length %d/%d exceeds %d", nA, nB, FFT_MAX_N);
   return THZ_OK;

@@ -772,6 +772,11 @@ static int czt_args(const thz_czt_desc64* d, CztArgs* a, size_t* total) {
   const double xo = d->outH * d->odx / 2.0, yo = d->outW * d->ody / 2.0;
   make(&a->pa, d->W, d->outH, -xo, xo);  // the reference's second Bluestein (:246): fx, outH
   make(&a->pb, d->H, d->outW, -yo, yo);  // its first (:243): fy, outW
+  // mp a power of two: the reference raises there (see thz_czt.hip czt_validate)
+  if (a->pa.np2 == a->pa.m + a->pa.M - 1 || a->pb.np2 == a->pb.m + a->pb.M - 1)
+    return fail(THZ_E_ARG, "CZT Bluestein length m + M - 1 is a power of two: the reference's slice "
+                           "b[m:mp+1] keeps M - 1 rows there and its product with h[m-1:mp] raises "
+                           "(Props/CZT_Prop.py:206,211)");
   if (a->pa.np2 > MAX_N || a->pb.np2 > MAX_N)
     return fail(THZ_E_UNSUPPORTED, "fp64 Bluestein length %d/%d exceeds %d", a->pa.np2, a->pb.np2, MAX_N);
   size_t off = 0;

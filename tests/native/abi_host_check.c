@@ -97,6 +97,24 @@ int main(void) {
   EXPECT(thz_czt_workspace_size(&c2, &ws) != THZ_OK, "czt non-square output");
   c2 = c; c2.wavelengths = NULL;
   EXPECT(thz_czt_workspace_size(&c2, &ws) != THZ_OK, "czt null wavelengths");
+  /* m + M - 1 a power of two (12 + 21 - 1 = 32): the reference's Bluestein slice raises there */
+  c2 = c; c2.H = 12; c2.W = 12; c2.outH = 21; c2.outW = 21;
+  EXPECT(thz_czt_workspace_size(&c2, &ws) == THZ_E_ARG && strstr(thz_last_error(), "power of two"),
+         "czt power-of-two Bluestein length refused");
+  c2.outH = 20; c2.outW = 20; /* 31: fine */
+  EXPECT(thz_czt_workspace_size(&c2, &ws) == THZ_OK, "czt Bluestein length 31 accepted");
+  c2.W = 13; /* the W pass: 13 + 20 - 1 = 32 */
+  EXPECT(thz_czt_workspace_size(&c2, &ws) == THZ_E_ARG, "czt power-of-two length on the W pass refused");
+  {
+    double wl64[1] = {1e-3};
+    thz_czt_desc64 c64;
+    memset(&c64, 0, sizeof c64);
+    c64.B = 1; c64.C = 1; c64.H = 12; c64.W = 12; c64.outH = 21; c64.outW = 21; c64.dx = 5e-4; c64.dy = 5e-4;
+    c64.odx = 2.5e-4; c64.ody = 2.5e-4; c64.z = 0.5; c64.wavelengths = wl64;
+    EXPECT(thz_czt64_workspace_size(&c64, &ws) == THZ_E_ARG, "fp64 czt power-of-two Bluestein length refused");
+    c64.outH = 20; c64.outW = 20;
+    EXPECT(thz_czt64_workspace_size(&c64, &ws) == THZ_OK, "fp64 czt Bluestein length 31 accepted");
+  }
   thz_rsc_desc r;
   memset(&r, 0, sizeof r);
   r.B = 1; r.C = 1; r.H = 64; r.W = 64; r.dx = 1e-3f; r.dy = 1e-3f; r.z = 0.3f; r.wavelengths = wl;

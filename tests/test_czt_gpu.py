@@ -42,6 +42,28 @@ def test_czt_rejects_non_square_output():
         P.czt_apply(x, [1e-3], [1e-3, 1e-3], 0.1, 16, 8, 1e-3, 1e-3)
 
 
+@pytest.mark.parametrize("H,W,M", [(12, 12, 21), (12, 13, 20), (16, 16, 1), (13, 12, 20)])
+def test_czt_power_of_two_bluestein_length_raises_like_the_reference(H, W, M):
+    """H + M - 1 or W + M - 1 a power of two: the reference's np2 equals mp, its slice b[m:mp+1]
+    keeps M - 1 rows and the product with h[m-1:mp] raises RuntimeError (Props/CZT_Prop.py:206,211;
+    the reference run here on these four shapes raised RuntimeError every time, MKL's FFT error for
+    M = 1).  The build raises RuntimeError (ThzError) before anything is launched, in fp32 and fp64,
+    where it used to leave the last output row unset (found by the randomized property sweep)."""
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.CZT_Prop import CZT_prop
+    dev = torch.device("cuda:0")
+    for dt, wl in ((torch.complex64, 1e-3), (torch.complex128, torch.tensor([1e-3], dtype=torch.float64))):
+        f = ElectricField(torch.ones(1, 1, H, W, dtype=dt, device=dev), wavelengths=wl, spacing=[0.5e-3, 0.6e-3],
+                          device=dev)
+        with pytest.raises(RuntimeError, match="power of two"):
+            CZT_prop(z_distance=0.5, device=dev)(f, M, M, 0.4e-3, 0.4e-3)
+    # one below: a valid length (12 + 20 - 1 = 31) runs and is finite
+    f = ElectricField(torch.ones(1, 1, 12, 12, dtype=torch.complex64, device=dev), wavelengths=1e-3,
+                      spacing=[0.5e-3, 0.6e-3], device=dev)
+    out = CZT_prop(z_distance=0.5, device=dev)(f, 20, 20, 0.4e-3, 0.4e-3).data
+    assert out.shape == (1, 1, 20, 20) and bool(torch.isfinite(out).all())
+
+
 @pytest.mark.parametrize("H,W,out,C", [(48, 64, 24, 2), (64, 64, 16, 1), (40, 36, 40, 1)])
 def test_czt_backward_vs_oracle_autograd(H, W, out, C):
     """CZT_prop backward (adjoint Bluestein kernels) vs autograd through the fp64 oracle."""

@@ -8,9 +8,13 @@ that hold for every input:
   z-summed adjoint of a multi-plane forward equals the sum of the per-plane adjoints;
 * agreement with the oracle on the drawn case (the fp64 restatement of the reference).
 
-Tolerances: fp32 rel 1e-5 for the identities (one fp32 pipeline each way), 1e-4 vs the fp64
-oracle; fp64 1e-12.
+Tolerances: fp32 rel 1e-5 for the identities (one fp32 pipeline each way); vs the fp64 oracle
+max(1e-4 (1 + k|z| / 1e3), 1.25 x the reference's own fp32 error on the drawn case); fp64 1e-12.
+Examples are derandomized, but which ones run can still differ between runs (hypothesis'
+generation depends on more than the seed), so every bound must hold for any draw.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -21,7 +25,10 @@ from oracle import thz_oracle as orc
 
 pytestmark = pytest.mark.gpu
 C0 = 2.998e8
-SETTINGS = settings(max_examples=50, deadline=None, derandomize=True,
+# THZ_PROP_EXAMPLES=<n> THZ_PROP_RANDOM=1: a wider, randomly seeded sweep (run by hand to shake out
+# bounds that only hold for the default draws)
+SETTINGS = settings(max_examples=int(os.environ.get("THZ_PROP_EXAMPLES", "50")), deadline=None,
+                    derandomize=os.environ.get("THZ_PROP_RANDOM", "0") != "1", database=None,
                     suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
 
 
@@ -74,10 +81,19 @@ def test_asm_properties(case):
     lhs = torch.vdot(out.detach().reshape(-1).to(torch.complex128), g.reshape(-1).to(torch.complex128))
     rhs = torch.vdot(x.reshape(-1).to(torch.complex128), gx.reshape(-1).to(torch.complex128))
     assert abs(complex(lhs - rhs)) <= 10 * tol * abs(complex(lhs)) + 1e-30
-    ref = orc.asm_forward(x.cpu().to(torch.complex128), lam32.double(),
-                          torch.tensor([case["dx"] * 1e-3] * 2, dtype=torch.float32).double(), z, case["s"],
-                          bandlimit=case["bl"] != "none", bandlimit_type="exact" if case["bl"] == "none" else case["bl"])
-    floor = 1e-11 if case["f64"] else 1e-4 * (1 + abs(z) * 2 * np.pi / float(lam32.min()) / 1e3)
+    sp32 = torch.tensor([case["dx"] * 1e-3] * 2, dtype=torch.float32)
+    kw = dict(bandlimit=case["bl"] != "none", bandlimit_type="exact" if case["bl"] == "none" else case["bl"])
+    ref = orc.asm_forward(x.cpu().to(torch.complex128), lam32.double(), sp32.double(), z, case["s"], **kw)
+    if case["f64"]:
+        floor = 1e-11
+    else:
+        # the reference's own fp32 error on this case (the oracle in fp32 = the reference's fp32
+        # arithmetic): near the evanescent cut-off of an unlimited band it reaches 2e-4 at k z ~ 1e3
+        # rad, so the bound is the larger of the phase-scaled 1e-4 and 1.25 x that error (the rule
+        # of tests/test_asm_gpu.py)
+        ref32 = orc.asm_forward(x.cpu().to(torch.complex64), lam32, sp32, z, case["s"], **kw)
+        e32 = float((ref32.to(torch.complex128) - ref).norm() / ref.norm())
+        floor = max(1e-4 * (1 + abs(z) * 2 * np.pi / float(lam32.min()) / 1e3), 1.25 * e32)
     assert float((Ax.cpu().to(torch.complex128) - ref).norm() / ref.norm()) <= floor
 
 
@@ -120,6 +136,12 @@ def test_czt_linearity_and_adjoint(case):
 
     shape = (1, 1, case["H"], case["W"])
     x, y = _rand(rng, shape, dt), _rand(rng, shape, dt)
+    if any(n & (n - 1) == 0 for n in (case["H"] + M - 1, case["W"] + M - 1)):
+        # a power-of-two Bluestein length: the reference raises RuntimeError there (its slice keeps
+        # M - 1 rows, Props/CZT_Prop.py:206,211), and so does this build
+        with pytest.raises(RuntimeError, match="power of two"):
+            A(x)
+        return
     lin = A(2 * x - 1j * y)
     ref = 2 * A(x) - 1j * A(y)
     assert float((lin - ref).norm() / ref.norm()) <= 10 * tol
