@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 tag=${1:-r03w}; n=${2:-400}; kexpr=${3:-}
 THZ_PROP_EXAMPLES=$n THZ_PROP_RANDOM=1 bash scripts/gpu_step.sh 1000 gpurun_out/${tag}_sweep.log \
-  python -u -m pytest tests/test_properties_gpu.py -v -m gpu --timeout 900 --timeout-method thread
+  python -u -m pytest tests/test_properties_gpu.py -v -m gpu --hypothesis-show-statistics --timeout 900 --timeout-method thread
 rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 if [ -n "$kexpr" ]; then

@@ -203,3 +203,43 @@ def test_rsc_linearity_adjoint_and_oracle(case):
         ref32 = orc.rsc_forward(x.cpu(), lam32, sp32, torch.tensor(case["z"], dtype=torch.float32))
         e32 = float((ref32.to(torch.complex128) - ref).norm() / ref.norm())
         assert e <= max(5e-4, 1.25 * e32), (e, e32)
+
+
+@SETTINGS
+@given(st.fixed_dictionaries({"hs": st.integers(1, 80), "ws": st.integers(1, 80), "up": st.integers(1, 3),
+                              "B": st.integers(1, 40), "C": st.integers(1, 4), "tol": st.sampled_from([0.0, 1e-5]),
+                              "seed": st.integers(0, 2 ** 31 - 1)}))
+def test_doe_modulate_vs_oracle(case):
+    """DOE modulate forward and both gradients (Components/QuantizedDOE.py:47-126: noise, nearest
+    upsampling of the height map to the field, transmission, product) vs the fp64 oracle's autograd
+    over drawn map / field sizes (up to 3x nearest upsampling, odd sizes), batch sizes 1..40 (every
+    batch-lane count of the backward's reduction) and 1..4 wavelengths: forward and field gradient
+    rel 2e-6, height gradient 1e-4 (fp32 sums over B C terms)."""
+    from quantizationawarethzdoe_amd import doe
+    from tests.golden_io import wavelengths
+    g = torch.Generator().manual_seed(case["seed"])
+    hs, ws, B, C = case["hs"], case["ws"], case["B"], case["C"]
+    H, W = hs * case["up"], ws * case["up"]
+    h = torch.rand(hs, ws, generator=g) * 1e-3
+    u = torch.rand(hs, ws, generator=g)
+    x = torch.randn(B, C, H, W, dtype=torch.complex64, generator=g)
+    go = torch.randn(B, C, H, W, dtype=torch.complex64, generator=g)
+    lam = wavelengths([240 + 30 * c for c in range(C)])
+    hd = h.to(_dev()).requires_grad_(True)
+    xd = x.to(_dev()).requires_grad_(True)
+    out, hfull = doe.modulate(xd, hd, [float(v) for v in lam], 2.66, 0.03, tolerance=case["tol"], noise=u.to(_dev()))
+    gx, gh = torch.autograd.grad(out, (xd, hd), grad_outputs=go.to(_dev()))
+    ho = h.double().requires_grad_(True)
+    xo = x.to(torch.complex128).requires_grad_(True)
+    ro = orc.doe_modulate(xo, ho, lam.double(), torch.tensor(2.66, dtype=torch.float64),
+                          torch.tensor(0.03, dtype=torch.float64), tolerance=case["tol"], noise_u01=u.double())
+    rgx, rgh = torch.autograd.grad(ro, (xo, ho), grad_outputs=go.to(torch.complex128))
+
+    def rel(a, b):
+        b = b.detach().numpy()
+        return float(np.linalg.norm(a.detach().cpu().numpy() - b) / max(np.linalg.norm(b), 1e-300))
+
+    assert hfull.shape == (H, W)
+    assert rel(out, ro) <= 2e-6
+    assert rel(gx, rgx) <= 2e-6
+    assert rel(gh, rgh) <= 1e-4
