@@ -23,6 +23,10 @@ def _f(v):
     return float(v.detach().cpu()) if torch.is_tensor(v) else float(v)
 
 
+def _pow2(n):
+    return n > 0 and n & (n - 1) == 0
+
+
 class CZT_prop(nn.Module):
     def __init__(self, z_distance: float = 0.0, device: str = None) -> None:
         super().__init__()
@@ -57,8 +61,15 @@ class CZT_prop(nn.Module):
         ody = sp[1] if outputPixel_dy is None else _f(outputPixel_dy)
         data = field.data
         x = _prop.kernel_dtype(data, "CZT_prop", field.wavelengths)
-        out = _CztFunction.apply(x, tuple(field.wavelengths_host), tuple(sp), self._zh, outputHeight, outputWidth,
-                                 odx, ody)
+        if outputHeight == outputWidth == 1 and _pow2(W) and not _pow2(H):
+            # the reference's second Bluestein pass (m = W, M = 1) has np2 = mp = W: its kept
+            # slice b[W:W+1] is empty and it returns a [B, C, 1, 0] field (Props/CZT_Prop.py:206,211;
+            # run here).  Every other power-of-two Bluestein length raises there, and the library
+            # refuses it (THZ_E_ARG -> RuntimeError).
+            out = x.new_zeros(x.shape[0], x.shape[1], 1, 0)
+        else:
+            out = _CztFunction.apply(x, tuple(field.wavelengths_host), tuple(sp), self._zh, outputHeight,
+                                     outputWidth, odx, ody)
         sp_out = [outputPixel_dx if outputPixel_dx is not None else field.spacing[0],
                   outputPixel_dy if outputPixel_dy is not None else field.spacing[1]]
         if all(torch.is_tensor(v) for v in sp_out):

@@ -57,6 +57,12 @@ def test_czt_power_of_two_bluestein_length_raises_like_the_reference(H, W, M):
                           device=dev)
         with pytest.raises(RuntimeError, match="power of two"):
             CZT_prop(z_distance=0.5, device=dev)(f, M, M, 0.4e-3, 0.4e-3)
+    # M = 1 with only the second pass's m = W a power of two: the reference returns a [B, C, 1, 0]
+    # field (run here: H, W = 5, 2 and 5, 1), so does the build
+    for w in (2, 1):
+        f = ElectricField(torch.ones(1, 1, 5, w, dtype=torch.complex64, device=dev), wavelengths=1e-3,
+                          spacing=[0.5e-3, 0.6e-3], device=dev)
+        assert tuple(CZT_prop(z_distance=0.5, device=dev)(f, 1, 1, 0.4e-3, 0.4e-3).data.shape) == (1, 1, 1, 0)
     # one below: a valid length (12 + 20 - 1 = 31) runs and is finite
     f = ElectricField(torch.ones(1, 1, 12, 12, dtype=torch.complex64, device=dev), wavelengths=1e-3,
                       spacing=[0.5e-3, 0.6e-3], device=dev)

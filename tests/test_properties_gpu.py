@@ -41,7 +41,7 @@ def _rand(rng, shape, dtype):
 
 
 asm_cases = st.fixed_dictionaries({
-    "B": st.integers(1, 2), "C": st.integers(1, 2), "H": st.integers(8, 160), "W": st.integers(8, 160),
+    "B": st.integers(1, 2), "C": st.integers(1, 2), "H": st.integers(1, 160), "W": st.integers(1, 160),
     "s": st.sampled_from([1, 1.5, 2]), "z": st.floats(0.005, 0.4), "neg": st.booleans(),
     "bl": st.sampled_from(["exact", "approx", "none"]), "f": st.floats(200.0, 400.0),
     "dx": st.sampled_from([0.5, 1.0]), "f64": st.booleans(), "seed": st.integers(0, 2 ** 31 - 1),
@@ -117,7 +117,7 @@ def test_asm_multi_plane_adjoint_is_the_sum_of_plane_adjoints(case):
 
 
 @SETTINGS
-@given(st.fixed_dictionaries({"H": st.integers(12, 96), "W": st.integers(12, 96), "M": st.integers(8, 64),
+@given(st.fixed_dictionaries({"H": st.integers(1, 96), "W": st.integers(1, 96), "M": st.integers(1, 64),
                               "z": st.floats(0.1, 0.6), "f64": st.booleans(), "seed": st.integers(0, 2 ** 31 - 1)}))
 def test_czt_linearity_and_adjoint(case):
     from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
@@ -136,9 +136,15 @@ def test_czt_linearity_and_adjoint(case):
 
     shape = (1, 1, case["H"], case["W"])
     x, y = _rand(rng, shape, dt), _rand(rng, shape, dt)
-    if any(n & (n - 1) == 0 for n in (case["H"] + M - 1, case["W"] + M - 1)):
+    p2 = [n & (n - 1) == 0 for n in (case["H"] + M - 1, case["W"] + M - 1)]
+    if M == 1 and p2[1] and not p2[0]:
+        # only the reference's second pass (m = W, M = 1) hits np2 == mp: it returns a [B, C, 1, 0]
+        # field there (run here), and so does this build
+        assert tuple(A(x).shape) == (1, 1, 1, 0)
+        return
+    if any(p2):
         # a power-of-two Bluestein length: the reference raises RuntimeError there (its slice keeps
-        # M - 1 rows, Props/CZT_Prop.py:206,211), and so does this build
+        # M - 1 rows, or an MKL error at M = 1; Props/CZT_Prop.py:206,211), and so does this build
         with pytest.raises(RuntimeError, match="power of two"):
             A(x)
         return
@@ -155,7 +161,7 @@ def test_czt_linearity_and_adjoint(case):
 
 
 @SETTINGS
-@given(st.fixed_dictionaries({"H": st.integers(8, 96), "W": st.integers(8, 96), "C": st.integers(1, 2),
+@given(st.fixed_dictionaries({"H": st.integers(1, 96), "W": st.integers(1, 96), "C": st.integers(1, 2),
                               "z": st.floats(0.05, 0.6), "f": st.floats(250.0, 400.0),
                               "dx": st.sampled_from([1.0, 1.2, 2.0]), "f64": st.booleans(),
                               "seed": st.integers(0, 2 ** 31 - 1)}))
