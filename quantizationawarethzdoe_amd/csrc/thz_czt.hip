@@ -27,7 +27,10 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <map>
 #include <mutex>
+#include <tuple>
+#include <vector>
 
 #include "thz_common.hpp"
 #include "thz_dev.hpp"
@@ -682,6 +685,102 @@ static int czt_lds_attr() {
 
 static int threads_pow2_or(int n) { return czt_pow2(n) ? n / pow2_v(n) : fft_threads(n); }
 
+// Per-device cache of a call's tables -- pre / post chirps and the filter spectra of both passes,
+// the workspace's leading table region -- keyed by everything they depend on (geometry, spacings,
+// z, wavelengths, direction): SURVEY §8(b)'s immutable per-device caches.  A repeated call with
+// the same key skips the six table launches (≈ 35 µs of a 0.85 ms cfg3 call).  Entries live for
+// the process; past CZT_TAB_MAX entries or bytes a call builds its tables in its workspace as
+// before, and so does a call made while its stream is being captured into a graph.
+struct CztTabKey {
+  int dev, adjoint, H, W, outH, outW, C;
+  float dx, dy, odx, ody, z;
+  std::vector<float> lam;
+  bool operator<(const CztTabKey& o) const {
+    return std::tie(dev, adjoint, H, W, outH, outW, C, dx, dy, odx, ody, z, lam) <
+           std::tie(o.dev, o.adjoint, o.H, o.W, o.outH, o.outW, o.C, o.dx, o.dy, o.odx, o.ody, o.z, o.lam);
+  }
+};
+struct CztTabEntry {
+  float2* buf;
+  hipEvent_t ready;  // recorded after the tables are built (another stream's call waits on it)
+};
+constexpr int CZT_TAB_MAX = 64;
+constexpr size_t CZT_TAB_MAX_BYTES = (size_t)512 << 20;
+static std::mutex g_tab_mu;
+static std::map<CztTabKey, CztTabEntry> g_tabs;
+static size_t g_tab_bytes = 0;
+
+static size_t czt_tab_bytes(const CztArgs& a, int C) {
+  size_t gend = (size_t)a.tabStride * C;
+  if (a.pa.nb) gend += (size_t)C * a.pa.nb * wf::N;
+  if (a.pb.nb) gend += (size_t)C * a.pb.nb * wf::N;
+  return a256(gend * sizeof(float2));
+}
+
+// Build the tables of one call into tab (its workspace, or a cache buffer).
+static int czt_build_tables(const CztArgs& a, const thz_czt_desc* d, float2* tab, hipStream_t s) {
+  int e;
+  {
+    KernelTimer kt("czt_tables", s);
+    const int nA = std::max({a.pa.m, a.pa.M, a.pa.np2}), nB = std::max({a.pb.m, a.pb.M, a.pb.np2});
+    hipLaunchKernelGGL(czt_tables, dim3((nA + 255) / 256, d->C), dim3(256), 0, s, a, tab, 0);
+    THZ_LAUNCH_CHECK();
+    hipLaunchKernelGGL(czt_tables, dim3((nB + 255) / 256, d->C), dim3(256), 0, s, a, tab, 1);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  // filter spectra in place, one launch per axis: FFT_np2(1/h) (one row per wavelength) or, for an
+  // overlap-add pass, FFT_1024 of each block's g_b (nb rows per wavelength)
+  const BluePass* ps[2] = {&a.pa, &a.pb};
+  const size_t fts[2] = {a.ftA, a.ftB};
+  for (int ax = 0; ax < 2; ++ax) {
+    const BluePass& p = *ps[ax];
+    if (p.nb) {
+      hipLaunchKernelGGL(czt_blk_tables, dim3(wf::N / 256, p.nb, d->C), dim3(256), 0, s, a, tab, ax);
+      THZ_LAUNCH_CHECK();
+      if ((e = fft_rows_strided(tab + fts[ax], tab + fts[ax], d->C * p.nb, wf::N, (size_t)wf::N, 0, s))) return e;
+    } else if ((e = fft_rows_strided(tab + fts[ax], tab + fts[ax], d->C, p.np2, (size_t)a.tabStride, 0, s))) {
+      return e;
+    }
+  }
+  return THZ_OK;
+}
+
+// The tables for this call: a cached buffer (built on first use), or its own workspace.
+static int czt_tables_for(const CztArgs& a, const thz_czt_desc* d, float2* ws, hipStream_t s, const float2** tab) {
+  *tab = ws;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  THZ_HIP_CHECK(hipStreamIsCapturing(s, &cs));
+  int dev = 0;
+  THZ_HIP_CHECK(hipGetDevice(&dev));
+  if (cs != hipStreamCaptureStatusNone) return czt_build_tables(a, d, ws, s);
+  CztTabKey k{dev, d->adjoint, d->H, d->W, d->outH, d->outW, d->C, d->dx, d->dy, d->odx, d->ody, d->z,
+              std::vector<float>(d->wavelengths, d->wavelengths + d->C)};
+  const size_t bytes = czt_tab_bytes(a, d->C);
+  std::lock_guard<std::mutex> lk(g_tab_mu);
+  auto it = g_tabs.find(k);
+  if (it != g_tabs.end()) {
+    THZ_HIP_CHECK(hipStreamWaitEvent(s, it->second.ready, 0));
+    *tab = it->second.buf;
+    return THZ_OK;
+  }
+  if ((int)g_tabs.size() >= CZT_TAB_MAX || g_tab_bytes + bytes > CZT_TAB_MAX_BYTES)
+    return czt_build_tables(a, d, ws, s);
+  CztTabEntry en{};
+  THZ_HIP_CHECK(hipMalloc(&en.buf, bytes));
+  int e = czt_build_tables(a, d, en.buf, s);
+  if (e == THZ_OK) e = hipEventCreateWithFlags(&en.ready, hipEventDisableTiming) == hipSuccess ? THZ_OK : THZ_E_HIP;
+  if (e == THZ_OK) e = hipEventRecord(en.ready, s) == hipSuccess ? THZ_OK : THZ_E_HIP;
+  if (e != THZ_OK) {
+    // the buffer may still be in use by launched work: keep it (leaked) rather than free it early
+    return e == THZ_E_HIP ? fail(THZ_E_HIP, "CZT table cache event") : e;
+  }
+  g_tabs.emplace(std::move(k), en);
+  g_tab_bytes += bytes;
+  *tab = en.buf;
+  return THZ_OK;
+}
+
 }  // namespace thz
 
 using namespace thz;
@@ -712,38 +811,16 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   if ((e = get_plan(a.pa.np2, &plA))) return e;
   if ((e = get_plan(a.pb.np2, &plB))) return e;
   hipStream_t s = (hipStream_t)stream;
-  float2* ws = (float2*)workspace;
   float2* V = (float2*)((char*)workspace + need - a256((size_t)a.BC * a.ncbA * CB * d->H * sizeof(float2)));
-  {
-    KernelTimer kt("czt_tables", s);
-    const int nA = std::max({a.pa.m, a.pa.M, a.pa.np2}), nB = std::max({a.pb.m, a.pb.M, a.pb.np2});
-    hipLaunchKernelGGL(czt_tables, dim3((nA + 255) / 256, d->C), dim3(256), 0, s, a, ws, 0);
-    THZ_LAUNCH_CHECK();
-    hipLaunchKernelGGL(czt_tables, dim3((nB + 255) / 256, d->C), dim3(256), 0, s, a, ws, 1);
-    THZ_LAUNCH_CHECK();
-    kt.stop();
-  }
-  // filter spectra in place, one launch per axis: FFT_np2(1/h) (one row per wavelength) or, for an
-  // overlap-add pass, FFT_1024 of each block's g_b (nb rows per wavelength)
-  const BluePass* ps[2] = {&a.pa, &a.pb};
-  const size_t fts[2] = {a.ftA, a.ftB};
-  for (int ax = 0; ax < 2; ++ax) {
-    const BluePass& p = *ps[ax];
-    if (p.nb) {
-      hipLaunchKernelGGL(czt_blk_tables, dim3(wf::N / 256, p.nb, d->C), dim3(256), 0, s, a, ws, ax);
-      THZ_LAUNCH_CHECK();
-      if ((e = fft_rows_strided(ws + fts[ax], ws + fts[ax], d->C * p.nb, wf::N, (size_t)wf::N, 0, s))) return e;
-    } else if ((e = fft_rows_strided(ws + fts[ax], ws + fts[ax], d->C, p.np2, (size_t)a.tabStride, 0, s))) {
-      return e;
-    }
-  }
+  const float2* ws = nullptr;  // the tables: cached, or built in the workspace's leading region
+  if ((e = czt_tables_for(a, d, (float2*)workspace, s, &ws))) return e;
   if (d->adjoint) {  // G [B, C, outW, outH] -> grad_in [B, C, H, W]: column pass first
     KernelTimer kt("czt_adjoint", s);
     THZ_CZT_SWITCH(a.pb.np2, czt_cols_adj, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
-                   fft_lds_bytes_io(a.pb.np2), s, (const float2*)in, V, (const float2*)ws, plB, a);
+                   fft_lds_bytes_io(a.pb.np2), s, (const float2*)in, V, ws, plB, a);
     THZ_LAUNCH_CHECK();
     THZ_CZT_SWITCH(a.pa.np2, czt_rows_adj, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
-                   fft_lds_bytes_io(a.pa.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plA, a);
+                   fft_lds_bytes_io(a.pa.np2), s, (const float2*)V, (float2*)out, ws, plA, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
     return THZ_OK;
@@ -752,10 +829,10 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
     KernelTimer kt("czt_rows", s);
     if (a.pa.nb) {
       hipLaunchKernelGGL(d->W % CZB_BS ? czt_rows_blk<true> : czt_rows_blk<false>, dim3((a.BC * d->H + CZB_W - 1) / CZB_W), dim3(64 * CZB_W), czb_lds_bytes(CZB_W), s,
-                         (const float2*)in, V, (const float2*)ws, a);
+                         (const float2*)in, V, ws, a);
     } else {
       THZ_CZT_SWITCH(a.pa.np2, czt_rows, dim3(a.BC * d->H), dim3(threads_pow2_or(a.pa.np2)),
-                     fft_lds_bytes_io(a.pa.np2), s, (const float2*)in, V, (const float2*)ws, plA, a);
+                     fft_lds_bytes_io(a.pa.np2), s, (const float2*)in, V, ws, plA, a);
     }
     THZ_LAUNCH_CHECK();
     kt.stop();
@@ -764,10 +841,10 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
     KernelTimer kt("czt_cols", s);
     if (a.pb.nb) {
       hipLaunchKernelGGL(d->H % CZB_BS ? czt_cols_blk<true> : czt_cols_blk<false>, dim3(a.BC * a.ncbA), dim3(64 * CZB_WC), czb_cols_lds_bytes(),
-                         s, (const float2*)V, (float2*)out, (const float2*)ws, a);
+                         s, (const float2*)V, (float2*)out, ws, a);
     } else {
       THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),
-                     fft_lds_bytes_io(a.pb.np2), s, (const float2*)V, (float2*)out, (const float2*)ws, plB, a);
+                     fft_lds_bytes_io(a.pb.np2), s, (const float2*)V, (float2*)out, ws, plB, a);
     }
     THZ_LAUNCH_CHECK();
     kt.stop();

@@ -446,6 +446,10 @@ def rsc_apply(data, wavelengths, spacing, z, vectorial=False, adjoint=False, fie
     else:
         Bo = 3 if vectorial else B
         out = torch.empty((Bo, C, 2 * (H // 2), 2 * (W // 2)), dtype=data.dtype, device=data.device)
+    if out.numel() == 0 or data.numel() == 0:
+        # H or W = 1: the reference's [..., H:, W:] window is empty (Props/RSC_Prop.py:203-207; run
+        # here: [B, C, 0, 2 (W // 2)] and the like); the adjoint of an empty output is zero
+        return out.zero_()
     with torch.cuda.device(data.device):
         _lib.check(run_fn(ctypes.byref(d), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(out.data_ptr()),
                           ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()), _stream_handle()))

@@ -179,3 +179,41 @@ def test_czt_cfg3_geometry_vs_reference_signature():
     assert out.shape == (1, 32, 512, 512)
     chk = bench.check_czt(out, idx)
     assert chk["ok"], chk
+
+
+def test_czt_table_cache_hits_and_graph_capture_match_fresh_tables():
+    """The per-device table cache (csrc/thz_czt.hip czt_tables_for): a first call builds a key's
+    tables into a cache buffer, later calls with the same key reuse them, a different z or
+    wavelength set is its own key, and a call captured into a HIP graph builds its tables in its
+    own workspace.  Every route gives bit-identical planes (the same table kernels either way),
+    forward and adjoint, on the overlap-add geometry and a np2 one."""
+    from quantizationawarethzdoe_amd import propagation as P
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(77)
+    for H, M in ((1100, 256), (96, 40)):
+        x = torch.randn(1, 2, H, H, dtype=torch.complex64, generator=g).to(dev)
+        z1, z2 = 0.2 + 1e-4 * H, 0.31 + 1e-4 * H  # keys no other test uses
+        wl = [1.01e-3, 1.2e-3]
+        args = ([0.5e-3, 0.5e-3], M, M, 0.35e-3, 0.35e-3)
+        a1 = P.czt_apply(x, wl, args[0], z1, *args[1:])          # builds z1's entry
+        b1 = P.czt_apply(x, wl, args[0], z2, *args[1:])          # z2's entry
+        a2 = P.czt_apply(x, wl, args[0], z1, *args[1:])          # hit
+        c1 = P.czt_apply(x, wl[::-1], args[0], z1, *args[1:])    # wavelengths swapped: own key
+        assert torch.equal(a1, a2) and not torch.equal(a1, b1)
+        assert torch.equal(c1[:, 0], P.czt_apply(x[:, :1].contiguous(), wl[1:], args[0], z1, *args[1:])[:, 0])
+        gy = torch.randn(a1.shape, dtype=torch.complex64, generator=g).to(dev)
+        adj1 = P.czt_apply(gy, wl, args[0], z1, *args[1:], adjoint=True, field_hw=(H, H))
+        adj2 = P.czt_apply(gy, wl, args[0], z1, *args[1:], adjoint=True, field_hw=(H, H))
+        assert torch.equal(adj1, adj2)
+        # captured: tables built inside the graph, in the call's workspace
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            P.czt_apply(x, wl, args[0], z1, *args[1:])
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = P.czt_apply(x, wl, args[0], z1, *args[1:])
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, a1)

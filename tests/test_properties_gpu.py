@@ -187,6 +187,10 @@ def test_rsc_linearity_adjoint_and_oracle(case):
 
     x, y = _rand(rng, (1, C, H, W), dt), _rand(rng, (1, C, H, W), dt)
     Ax, Ay = A(x), A(y)
+    if min(H, W) == 1:
+        # the reference's [..., H:, W:] window of a 1-pixel axis is empty (run here), and so is this
+        assert tuple(Ax.shape) == (1, C, 2 * (H // 2), 2 * (W // 2)) and Ax.numel() == 0
+        return
     lin = A(2 * x - 1j * y)
     assert float((lin - (2 * Ax - 1j * Ay)).norm() / (2 * Ax - 1j * Ay).norm()) <= 10 * tol
     xg = x.clone().requires_grad_(True)

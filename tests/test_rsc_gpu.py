@@ -140,3 +140,20 @@ def test_vrs_forward_backward_vs_golden(case, capsys):
     assert capsys.readouterr().out.strip() == case["stdout"]
     out.backward(torch.from_numpy(A[f"{k}__gout"]).to(dev))
     assert rel_l2(data.grad.cpu().numpy(), A[f"{k}__gin64"]) <= 5e-4
+
+
+@pytest.mark.parametrize("H,W", [(1, 1), (1, 3), (3, 1), (2, 1)])
+def test_rsc_one_pixel_axis_gives_the_reference_empty_window(H, W):
+    """A field with a 1-pixel axis: the reference's window [..., H:, W:] of the P = H + 2 floor(H/2)
+    grid is empty on that axis (the reference run here: [1, 1, 0, 0] for 1 x 1, [1, 1, 0, 2] for
+    1 x 3, [1, 1, 2, 0] for 3 x 1 and 2 x 1).  The build returns the same empty field without a
+    launch, and its backward is a zero gradient."""
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.RSC_Prop import RSC_prop
+    dev = torch.device("cuda:0")
+    x = torch.ones(1, 1, H, W, dtype=torch.complex64, device=dev, requires_grad=True)
+    out = RSC_prop(z_distance=0.5, device=dev)(ElectricField(x, wavelengths=1e-3, spacing=[1e-3, 1.1e-3],
+                                                              device=dev)).data
+    assert tuple(out.shape) == (1, 1, 2 * (H // 2), 2 * (W // 2)) and out.numel() == 0
+    out.sum().abs().backward()
+    assert x.grad is not None and bool((x.grad == 0).all())
