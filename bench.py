@@ -276,12 +276,14 @@ def check_qat(dev):
 def bench_qat(dev, rank, world, steps=60, dist=None):
     """cfg4 (secondary line): four-focal-spots QAT iterations/s in each schedule phase (iter_frac
     <= 0.3 continuous, 0.3-0.8 blend, > 0.8 quantized), with the one-bucket gradient all-reduce
-    across ranks (each rank its own noise sample).  Afterwards the reference's 20-step trace is
+    across ranks (each rank its own noise sample; on RCCL captured inside the step's HIP graph, so
+    a step is one replay).  Afterwards the reference's 20-step trace is
     replayed through the same kernels (check_qat)."""
     from quantizationawarethzdoe_amd import qat
     torch.manual_seed(1234 + rank)
     system = qat.FourFocalSpotsSystem(device=dev)
-    trainer = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=6000, graph=True)
+    trainer = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=6000, graph=True,
+                             capture_collective=True)
     out = {}
     for name, frac in (("continuous", 0.1), ("blend", 0.5), ("quantized", 0.9)):
         for _ in range(5):
@@ -301,7 +303,8 @@ def bench_qat(dev, rank, world, steps=60, dist=None):
         out[name] = {"it_per_s": round(steps / dt, 1), "ms_per_it": round(dt / steps * 1e3, 3),
                      "loss": round(float(loss.detach()), 6)}
     return {"workload": "cfg4: four_focal_spots QAT step (v3 DOE 100^2, ASM P=300, fused loss, Adam), "
-                        "HIP-graph replay per schedule phase, gradient all-reduce over ranks", "phases": out,
+                        "HIP-graph replay per schedule phase, gradient all-reduce over ranks (RCCL: inside the graph)",
+            "graph_collective": bool(trainer.allreduce.capturable and trainer.capture_collective), "phases": out,
             "output_check": check_qat(dev)}
 
 
@@ -359,7 +362,7 @@ def bench_donn(dev, rank, world, steps=20, warmup=3, dist=None):
         torch.manual_seed(1234)  # same initial weights on every rank
         model = donn.DONN(device=dev)
         torch.manual_seed(1234 + rank)  # per-rank height-noise draws
-        tr = donn.DONNTrainer(model, targets, graph=True, chained=chained)
+        tr = donn.DONNTrainer(model, targets, graph=True, chained=chained, capture_collective=True)
         for _ in range(warmup):
             tr.step(u, labels)
         torch.cuda.synchronize()
@@ -375,6 +378,7 @@ def bench_donn(dev, rank, world, steps=20, warmup=3, dist=None):
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         out[name] = {"samples_per_s": round(256 * steps / dt, 1), "ms_per_step": round(dt / steps * 1e3, 3),
+                     "graph_collective": bool(tr.allreduce.capturable and tr.capture_collective),
                      "loss": round(float(loss.detach()), 6), "output_check": check_donn(dev, chained)}
     return {"workload": "cfg5: 3-layer DONN (100^2, P=300 ASM, FullPrecision DOE layers) training step, global "
                         "batch 256 split over ranks, detector-target loss, gradient all-reduce, Adam, HIP-graph "

@@ -141,7 +141,7 @@ class DONNTrainer:
     """
 
     def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True, loss_fn=None,
-                 device_rng=True):
+                 device_rng=True, capture_collective=False, force_collective=False):
         from quantizationawarethzdoe_amd.qat import GradientAllReduce
         self.model = model
         self.targets = targets.to(model.device).float().contiguous()
@@ -152,7 +152,8 @@ class DONNTrainer:
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph,
                                           fused=bool(self.params) and self.params[0].is_cuda)
-        self.allreduce = GradientAllReduce(self.params, group=group)
+        self.allreduce = GradientAllReduce(self.params, group=group, force=force_collective)
+        self.capture_collective = bool(capture_collective)  # qat.QATTrainer's option
         self._one = torch.ones((), dtype=torch.float32, device=model.device)
         self.itr = 0
         self._graphs = {}
@@ -212,9 +213,10 @@ class DONNTrainer:
         side.wait_stream(torch.cuda.current_stream())
         with self._step_state.installed(self.model.does):
             with torch.cuda.stream(side):
-                for _ in range(2):  # allocator, autograd and Adam's lazy state, outside the capture
+                for _ in range(2):  # allocator, autograd, Adam's lazy state, communicator: outside the capture
                     self.optimizer.zero_grad(set_to_none=True)
                     self._fb(su, st, frac)
+                    self.allreduce.reduce()
                     self._opt()
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
@@ -227,13 +229,22 @@ class DONNTrainer:
                         if torch.is_tensor(v):
                             v.copy_(saved[k]) if saved is not None else v.zero_()
             self.optimizer.zero_grad(set_to_none=True)
-            if self.allreduce.world == 1:
-                # no collective: the whole step (fwd/bwd, Adam) is one graph, one replay per step
-                g_fb = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g_fb):
-                    loss = self._fb(su, st, frac)
-                    self._opt()
-                return g_fb, None, loss
+            if not self.allreduce.active or (self.capture_collective and self.allreduce.capturable):
+                # no collective, or a captured one: the whole step is one graph, one replay per step
+                try:
+                    g_fb = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_fb):
+                        loss = self._fb(su, st, frac)
+                        self.allreduce.reduce()
+                        self._opt()
+                    return g_fb, None, loss
+                except RuntimeError as e:
+                    if not self.allreduce.active:
+                        raise
+                    from quantizationawarethzdoe_amd.qat import _warn_capture
+                    _warn_capture(e)  # same code on every rank: all of them fall back together
+                    self.capture_collective = False
+                    self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb):
                 loss = self._fb(su, st, frac)
@@ -255,7 +266,7 @@ class DONNTrainer:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
         g_fb.replay()
-        if g_opt is not None:  # world > 1: the collective between the two captured halves
+        if g_opt is not None:  # an eager collective between the two captured halves
             self.allreduce.reduce()
             g_opt.replay()
         return loss

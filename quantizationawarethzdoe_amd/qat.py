@@ -159,6 +159,12 @@ class StepState:
                 d.__dict__.pop("_rng", None)
 
 
+def _warn_capture(e):
+    import warnings
+    warnings.warn(f"capturing the gradient all-reduce into the step graph failed ({e}); "
+                  "falling back to split graphs around an eager all-reduce", RuntimeWarning)
+
+
 class GradientAllReduce:
     """Average the gradients of ``params`` over the process group with ONE flat all-reduce.
 
@@ -167,20 +173,24 @@ class GradientAllReduce:
     put ``pack`` at the end of the captured forward/backward graph, ``reduce`` (the collective)
     between the graph replays and ``unpack`` at the head of the optimiser graph -- the same
     calls the eager step makes, so the CPU gloo tests run the exact placement the HIP-graph
-    path replays.  All three are no-ops at world size 1.
+    path replays.  All three are no-ops at world size 1 unless ``force`` (an initialised process
+    group of one rank: the collective still runs, to test and time its capture on one GPU).
     """
 
-    def __init__(self, params, group=None):
+    def __init__(self, params, group=None, force=False):
         self.params = [p for p in params if p.requires_grad]
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.active = self.world > 1 or (bool(force) and dist.is_available() and dist.is_initialized())
+        # the collective can be captured into a HIP graph on RCCL (torch's "nccl" backend) only
+        self.capturable = self.active and dist.get_backend(group) == "nccl"
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
 
     def pack(self):
         """Gradients -> the flat bucket (a parameter without a gradient contributes zeros)."""
-        if self.world == 1:
+        if not self.active:
             return
         off = 0
         for p in self.params:
@@ -193,14 +203,14 @@ class GradientAllReduce:
 
     def reduce(self):
         """The one collective of the step: sum over ranks, then / world."""
-        if self.world == 1:
+        if not self.active:
             return
         dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
         self.flat.mul_(1.0 / self.world)
 
     def unpack(self):
         """The averaged bucket -> every parameter's gradient."""
-        if self.world == 1:
+        if not self.active:
             return
         off = 0
         for p in self.params:
@@ -228,12 +238,14 @@ class QATTrainer:
     the quantizer kernels through a 3-float device buffer (thz_quant_desc.dyn), and the
     Gumbel / height-noise draws are graph-safe philox draws, so each replay is a fresh sample.
     On one rank the whole step (forward, loss, backward, Adam) is ONE graph; with N ranks the
-    replay is split around the (eager) gradient all-reduce.  The random stream differs from the
-    eager path (same distribution, different draws).
+    replay is split around the (eager) gradient all-reduce, or, with ``capture_collective``, the
+    all-reduce is captured too and the step is again one replay (RCCL kernels inside the graph).
+    The random stream differs from the eager path (same distribution, different draws).
+    ``force_collective`` runs the collective on a one-rank process group (tests / timing).
     """
 
     def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False, loss_fn=None,
-                 device_rng=True):
+                 device_rng=True, capture_collective=False, force_collective=False):
         self.system = system
         self.target = target.to(system.device).float().contiguous()
         self.max_itrs = max_itrs
@@ -244,7 +256,8 @@ class QATTrainer:
         # one fused Adam kernel per step on the GPU (torch's multi-tensor path launches ~7 small kernels)
         self.optimizer = torch.optim.Adam(params, lr=lr, capturable=graph,
                                           fused=bool(params) and params[0].is_cuda)
-        self.allreduce = GradientAllReduce(list(system.parameters()), group=group)
+        self.allreduce = GradientAllReduce(list(system.parameters()), group=group, force=force_collective)
+        self.capture_collective = bool(capture_collective)
         self._one = torch.ones((), dtype=torch.float32, device=system.device)
         self.itr = 0
         self._graphs = {}
@@ -306,6 +319,7 @@ class QATTrainer:
                 for _ in range(2):
                     self.optimizer.zero_grad(set_to_none=True)
                     self._fb(frac)
+                    self.allreduce.reduce()  # the communicator is set up outside the capture
                     self._opt()
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
@@ -318,13 +332,22 @@ class QATTrainer:
                         if torch.is_tensor(v):
                             v.copy_(saved[k]) if saved is not None else v.zero_()
             self.optimizer.zero_grad(set_to_none=True)
-            if self.allreduce.world == 1:
-                # no collective: the whole step (fwd/bwd, Adam) is one graph, one replay per step
-                g_fb = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g_fb):
-                    loss = self._fb(frac)
-                    self._opt()
-                return g_fb, None, loss
+            if not self.allreduce.active or (self.capture_collective and self.allreduce.capturable):
+                # no collective, or a captured one: the whole step (fwd/bwd, all-reduce, Adam) is
+                # one graph, one replay per step
+                try:
+                    g_fb = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g_fb):
+                        loss = self._fb(frac)
+                        self.allreduce.reduce()
+                        self._opt()
+                    return g_fb, None, loss
+                except RuntimeError as e:
+                    if not self.allreduce.active:
+                        raise
+                    _warn_capture(e)  # same code on every rank: all of them fall back together
+                    self.capture_collective = False
+                    self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb):
                 loss = self._fb(frac)
@@ -339,7 +362,7 @@ class QATTrainer:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
         g_fb.replay()
-        if g_opt is not None:  # world > 1: the collective between the two captured halves
+        if g_opt is not None:  # an eager collective between the two captured halves
             self.allreduce.reduce()
             g_opt.replay()
         return loss

@@ -1,0 +1,85 @@
+"""The gradient all-reduce captured inside the step's HIP graph (``capture_collective``), on a
+one-rank RCCL process group with the collective forced on (``force_collective``): the step is
+then ONE replay with the RCCL all-reduce kernel inside it, instead of the fwd/bwd replay, an eager
+all-reduce and the optimiser replay.  Same trajectory bit for bit as the split form (a one-rank
+sum is the identity), for the QAT (cfg4) and DONN (cfg5) trainers; the per-step times of both
+forms are printed (-s) for the record.  Multi-rank capture needs more than the one GPU a test box
+has; the eager split form stays the default."""
+import socket
+import time
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.fixture(scope="module")
+def one_rank_rccl():
+    import torch.distributed as dist
+    if dist.is_initialized():
+        pytest.skip("a process group is already initialised in this process")
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=torch.device("cuda:0"))
+    try:
+        yield dist
+    finally:
+        dist.destroy_process_group()
+
+
+def _time_steps(step, n=200):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e3
+
+
+def test_qat_captured_allreduce_matches_split_graphs(one_rank_rccl):
+    from quantizationawarethzdoe_amd import qat
+    dev = torch.device("cuda:0")
+    res = {}
+    for capture in (False, True):
+        torch.manual_seed(5)
+        system = qat.FourFocalSpotsSystem(device=dev)
+        tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), graph=True, force_collective=True,
+                            capture_collective=capture)
+        assert tr.allreduce.active and tr.allreduce.world == 1
+        losses = [float(tr.step(f)) for f in np.linspace(0.0, 0.95, 30)]
+        w = next(iter(system.parameters())).detach().clone()
+        ms = _time_steps(lambda: tr.step(0.9))
+        res[capture] = (losses, w, ms)
+        assert all(g is None for _, g, _ in tr._graphs.values()) == capture  # one replay per step
+    assert res[False][0] == res[True][0] and torch.equal(res[False][1], res[True][1])
+    print(f"\ncfg4 QAT step, one-rank RCCL all-reduce: split graphs + eager collective {res[False][2]:.4f} ms, "
+          f"captured {res[True][2]:.4f} ms")
+
+
+def test_donn_captured_allreduce_matches_split_graphs(one_rank_rccl):
+    from quantizationawarethzdoe_amd import donn
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(3)
+    u = torch.rand(32, 1, 100, 100, generator=g).to(dev)
+    labels = torch.randint(0, 10, (32,), generator=g).to(dev)
+    targets = donn.detector_targets(device=dev)
+    res = {}
+    for capture in (False, True):
+        torch.manual_seed(7)
+        model = donn.DONN(device=dev)
+        tr = donn.DONNTrainer(model, targets, graph=True, force_collective=True, capture_collective=capture)
+        losses = [float(tr.step(u, labels)) for _ in range(8)]
+        ws = [p.detach().clone() for p in tr.params]
+        ms = _time_steps(lambda: tr.step(u, labels), n=50)
+        res[capture] = (losses, ws, ms)
+    assert res[False][0] == res[True][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[False][1], res[True][1]))
+    print(f"\ncfg5 DONN step (batch 32), one-rank RCCL all-reduce: split {res[False][2]:.4f} ms, "
+          f"captured {res[True][2]:.4f} ms")
