@@ -502,7 +502,9 @@ __device__ __forceinline__ int radial_bin(int i, int j, int R, int H, int W) {
   const int qx = fi < R ? R - 1 - fi : fi - R;
   const int qy = fj < R ? R - 1 - fj : fj - R;
   const float d = sqrtf((float)(qx * qx + qy * qy));
-  return d < (float)(R - 1) ? (int)floorf(d) : -1;
+  // bin 0 (r < 1) is filled for every R, bins k >= 1 for r < R - 1 (:1421-1423): at R = 1 the
+  // single quadrant pixel still takes profile[0]
+  return d < fmaxf(1.0f, (float)(R - 1)) ? (int)floorf(d) : -1;
 }
 
 __global__ void radial_fwd(const float* __restrict__ prof, float* __restrict__ out, int R, int H, int W) {
@@ -521,7 +523,7 @@ __global__ void radial_bwd(const float* __restrict__ g, float* __restrict__ gpro
 }  // namespace thz
 
 extern "C" int thz_radial_forward(const float* profile, int R, int H, int W, float* out, thz_stream_t stream) {
-  if (!profile || !out || R < 2 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
+  if (!profile || !out || R < 1 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
     return fail(THZ_E_ARG, "bad radial map arguments R=%d H=%d W=%d", R, H, W);
   hipLaunchKernelGGL(radial_fwd, dim3((H * W + 255) / 256), dim3(256), 0, (hipStream_t)stream, profile, out, R, H, W);
   THZ_LAUNCH_CHECK();
@@ -530,7 +532,7 @@ extern "C" int thz_radial_forward(const float* profile, int R, int H, int W, flo
 
 extern "C" int thz_radial_backward(const float* grad_out, int R, int H, int W, float* grad_profile,
                                    thz_stream_t stream) {
-  if (!grad_out || !grad_profile || R < 2 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
+  if (!grad_out || !grad_profile || R < 1 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
     return fail(THZ_E_ARG, "bad radial map arguments");
   hipStream_t s = (hipStream_t)stream;
   THZ_HIP_CHECK(hipMemsetAsync(grad_profile, 0, sizeof(float) * R, s));

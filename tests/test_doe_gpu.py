@@ -244,7 +244,7 @@ def test_sgv3_quantizer_vs_oracle_256(iter_frac, mirror):
 
 def test_radial_map_odd_sizes():
     from quantizationawarethzdoe_amd import doe
-    for H, W in [(32, 32), (31, 33), (100, 100), (7, 9)]:
+    for H, W in [(32, 32), (31, 33), (100, 100), (7, 9), (2, 2), (3, 2)]:  # 2 x 2: R = 1, bin 0 only
         R = int(max(H, W) * np.sqrt(2) / 2)
         prof = torch.rand(R, dtype=torch.float32)
         ref = orc.radial_map(prof, R, H, W)
