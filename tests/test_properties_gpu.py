@@ -288,7 +288,7 @@ def test_doe_layer_vs_oracle(case):
     v2 / v3 and the five rotationally symmetric ones) over drawn DOE sizes (odd ones included), a
     mirrored unit cell or not, 2..8 levels, height limits, schedule positions and weight scales, with
     the Gumbel and height-noise draws injected: the layer's height map vs the oracle's in fp32
-    (QuantizedDOE.py:286-1623 restated, the reference's arithmetic) to 1e-6 -- a LUT pick may flip
+    (QuantizedDOE.py:286-1623 restated, the reference's arithmetic) to 5e-6 -- a LUT pick may flip
     where two perturbed scores tie to fp32 rounding, at most one pixel, and then the gradient is not
     compared -- and the weight gradient of sum |out|^2 through the modulated field vs the oracle's
     fp64 autograd within max(1e-4, 1.5 x the reference's own fp32 error) rel-L2."""
@@ -342,7 +342,10 @@ def test_doe_layer_vs_oracle(case):
                               2 if unit else None, [n, n], expo=draws.get("expo"))
     hn = layer.height_map.detach().cpu()
     assert tuple(hn.shape) == tuple(ho.shape) == (n, n)
-    mism = int((~torch.isclose(hn, ho.detach(), rtol=1e-6, atol=1e-12)).sum())
+    # 5e-6: the smooth maps (FP, PSQ's sum of L sigmoids, the v3 blend) carry a few fp32 ulps of
+    # their own (the reference's fp32 is 8e-7 from fp64 on a drawn PSQ map); a LUT flip is a
+    # whole level step, >= hmax / 8
+    mism = int((~torch.isclose(hn, ho.detach(), rtol=5e-6, atol=1e-12)).sum())
     assert mism <= 1, mism
     if mism:
         return
