@@ -372,3 +372,65 @@ def test_doe_layer_vs_oracle(case):
         # the largest off by 5 %); a wrong formula is off by O(1) on the largest elements
         e32 = float((g32 - g64).norm() / g64.norm())
         assert float((gn - g64).norm() / g64.norm()) <= max(2e-4, 3 * e32), e32
+
+
+@SETTINGS
+@given(st.fixed_dictionaries({"H": st.integers(2, 96), "W": st.integers(2, 96), "B": st.integers(1, 3),
+                              "C": st.integers(1, 2), "dx": st.sampled_from([0.5e-3, 1e-3, 1.3e-3]),
+                              "dy": st.sampled_from([0.5e-3, 1e-3, 0.7e-3]), "f": st.floats(0.05, 0.5),
+                              "kind": st.sampled_from(["rect", "circ"]), "size": st.floats(2e-3, 0.12),
+                              "Ho": st.integers(1, 96), "Wo": st.integers(1, 96),
+                              "zoom": st.sampled_from([0.25, 0.5, 1.0, 1.7, 3.0]), "seed": st.integers(0, 2 ** 31 - 1)}))
+def test_optics_elements_vs_oracle(case):
+    """Thin lens (Components/Thin_Lens.py:31-85), aperture masks (Components/Aperture.py:61-118) and
+    the field resampler (Addons/Field_Resampler.py:56-118) over drawn shapes, spacings, focal
+    lengths, aperture sizes and output grids: the lens within max(2e-6, 1.5 x the reference's fp32
+    error) of the fp64 oracle (its phase pi r^2 / (lambda f) reaches ~10^3 rad here), the aperture
+    bit-exact against the oracle's fp32 mask, the resampler and its gradient within 1e-5 of the
+    oracle's fp32 grid_sample (bilinear weights rounded in another order)."""
+    from quantizationawarethzdoe_amd.Addons.Field_Resampler import Field_Resampler
+    from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
+    from quantizationawarethzdoe_amd.Components.Thin_Lens import Thin_LensElement
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from tests.golden_io import wavelengths
+    g = torch.Generator().manual_seed(case["seed"])
+    B, C, H, W = case["B"], case["C"], case["H"], case["W"]
+    lam = wavelengths([300 + 25 * c for c in range(C)])
+    x = torch.randn(B, C, H, W, dtype=torch.complex64, generator=g)
+    dx, dy = case["dx"], case["dy"]
+
+    def ef(data):
+        return ElectricField(data, wavelengths=[float(v) for v in lam] if C > 1 else float(lam[0]),
+                             spacing=[dx, dy], device=_dev())
+
+    def rel(a, b):
+        a, b = a.detach().cpu().to(torch.complex128), b.detach().to(torch.complex128)
+        return float((a - b).norm() / max(float(b.norm()), 1e-300))
+
+    sp32 = torch.tensor([dx, dy], dtype=torch.float32)
+    # thin lens
+    lens = Thin_LensElement(case["f"])(ef(x.to(_dev()))).data
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        r64 = orc.thin_lens(x.to(torch.complex128), float(sp32[0]), float(sp32[1]), case["f"], lam.double())
+    finally:
+        torch.set_default_dtype(prev)
+    r32 = orc.thin_lens(x, float(sp32[0]), float(sp32[1]), case["f"], lam)
+    assert rel(lens, r64) <= max(2e-6, 1.5 * rel(r32, r64))
+    # aperture
+    ap = ApertureElement(case["kind"], case["size"])(ef(x.to(_dev()))).data
+    mask = orc.aperture_mask(H, W, float(sp32[0]), float(sp32[1]), case["kind"], case["size"])
+    assert torch.equal(ap.cpu(), x * mask)
+    # resampler, forward and gradient
+    Ho, Wo = case["Ho"], case["Wo"]
+    dxo, dyo = dx / case["zoom"], dy / case["zoom"]
+    xd = x.to(_dev()).requires_grad_(True)
+    out = Field_Resampler(Ho, Wo, dxo, dyo)(ef(xd)).data
+    gout = torch.randn(out.shape, dtype=torch.complex64, generator=g)
+    gx, = torch.autograd.grad(out, xd, grad_outputs=gout.to(_dev()))
+    xo = x.clone().requires_grad_(True)
+    ro = orc.resample(xo, [float(sp32[0]), float(sp32[1])], Ho, Wo, float(np.float32(dxo)), float(np.float32(dyo)))
+    rgx, = torch.autograd.grad(ro, xo, grad_outputs=gout)
+    assert tuple(out.shape) == tuple(ro.shape)
+    assert rel(out, ro) <= 1e-5 and rel(gx, rgx) <= 1e-5
