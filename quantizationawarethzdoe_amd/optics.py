@@ -194,4 +194,12 @@ def resample(x, Hout, Wout, dx_in, dy_in, dx_out, dy_out):
     output pixel pitch (Addons/Field_Resampler.py:74-118), differentiable."""
     if x.dtype != torch.complex64:
         raise TypeError(f"resampler kernel computes in complex64; got {x.dtype}")
+    H, W = x.shape[-2:]
+    if (H - 1) // 2 == 0 or (W - 1) // 2 == 0:
+        # fewer than 3 pixels on an axis: the reference normalises the sampling grid by
+        # dx ((H - 1) // 2) = 0 and grid_sample returns NaN everywhere (run here on 1 x 4, 2 x 2 and
+        # 2 x 5 fields); the same NaN field, still attached to the input for autograd
+        out = torch.full((*x.shape[:-2], int(Hout), int(Wout)), complex(float("nan"), float("nan")),
+                         dtype=x.dtype, device=x.device)
+        return out + 0 * x.sum(dim=(-2, -1), keepdim=True) if x.requires_grad else out
     return _Resample.apply(x, int(Hout), int(Wout), float(dx_in), float(dy_in), float(dx_out), float(dy_out))
