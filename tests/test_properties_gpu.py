@@ -349,10 +349,10 @@ def test_doe_layer_vs_oracle(case):
     assert mism <= 1, mism
     if mism:
         return
-    def oracle_grad(dt):
+    def oracle_grad(dt, wscale=1.0):
         """d sum |out|^2 / d weight: the layer in dt (float32 = the reference's arithmetic), the
-        modulation in fp64"""
-        w = w0.clone().to(dt).requires_grad_(True)
+        modulation in fp64; wscale perturbs the weights by a few ulps"""
+        w = (w0.clone().to(dt) * wscale).requires_grad_(True)
         e = draws.get("expo")
         h = orc.layer_height_map(cls, w, lut.to(dt), torch.tensor(case["hmax"], dtype=dt), lam.min().to(dt), 2.66,
                                  frac, optim, 2 if unit else None, [n, n], expo=None if e is None else e.to(dt))
@@ -370,8 +370,12 @@ def test_doe_layer_vs_oracle(case):
         # fp32 error on the drawn case -- 0.7 % was drawn at a 2 x 2 v2 map (this build 0.2 %), and
         # 4.3e-5 at a 37 x 37 rotationally symmetric v3 map (this build 1.04e-4, from elements 1e-3 of
         # the largest off by 5 %); a wrong formula is off by O(1) on the largest elements
+        # and by the spread of the reference's fp32 arithmetic under a 2-ulp weight perturbation
+        # (the conditioning of the drawn case: 0.6 % drawn at a saturated 2 x 2 rotationally
+        # symmetric v3 map whose fp32 reference happened to land 0.06 % from fp64)
         e32 = float((g32 - g64).norm() / g64.norm())
-        assert float((gn - g64).norm() / g64.norm()) <= max(2e-4, 3 * e32), e32
+        ep = max(float((oracle_grad(torch.float32, 1.0 + k * 2.0 ** -22) - g64).norm() / g64.norm()) for k in (1, -1))
+        assert float((gn - g64).norm() / g64.norm()) <= max(2e-4, 3 * e32, 3 * ep), (e32, ep)
 
 
 @SETTINGS
