@@ -390,8 +390,8 @@ def test_optics_elements_vs_oracle(case):
     the field resampler (Addons/Field_Resampler.py:56-118) over drawn shapes, spacings, focal
     lengths, aperture sizes and output grids: the lens within max(4e-6, 2 x the reference's fp32
     error) of the fp64 oracle (its phase pi r^2 / (lambda f) reaches ~10^3 rad here), the aperture
-    bit-exact against the oracle's fp32 mask, the resampler and its gradient within 3e-5 of the
-    oracle's fp32 grid_sample (bilinear weights rounded in another order)."""
+    bit-exact against the oracle's fp32 mask, the resampler and its gradient within max(1e-5, 3 x
+    the reference's fp32 error) of the oracle's fp64 grid_sample."""
     from quantizationawarethzdoe_amd.Addons.Field_Resampler import Field_Resampler
     from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
     from quantizationawarethzdoe_amd.Components.Thin_Lens import Thin_LensElement
@@ -441,14 +441,26 @@ def test_optics_elements_vs_oracle(case):
     out = Field_Resampler(Ho, Wo, dxo, dyo)(ef(xd)).data
     gout = torch.randn(out.shape, dtype=torch.complex64, generator=g)
     gx, = torch.autograd.grad(out, xd, grad_outputs=gout.to(_dev()))
-    xo = x.clone().requires_grad_(True)
-    ro = orc.resample(xo, [float(sp32[0]), float(sp32[1])], Ho, Wo, float(np.float32(dxo)), float(np.float32(dyo)))
-    rgx, = torch.autograd.grad(ro, xo, grad_outputs=gout)
-    assert tuple(out.shape) == tuple(ro.shape)
+    def oracle_resample(dt):
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(torch.float64 if dt == torch.complex128 else torch.float32)
+        try:
+            xo = x.clone().to(dt).requires_grad_(True)
+            ro = orc.resample(xo, [float(sp32[0]), float(sp32[1])], Ho, Wo, float(np.float32(dxo)),
+                              float(np.float32(dyo)))
+            rgx, = torch.autograd.grad(ro, xo, grad_outputs=gout.to(dt))
+        finally:
+            torch.set_default_dtype(prev)
+        return ro.detach(), rgx
+
+    r32, rg32 = oracle_resample(torch.complex64)
+    r64, rg64 = oracle_resample(torch.complex128)
+    assert tuple(out.shape) == tuple(r32.shape)
     if min(H, W) < 3:
         # the reference's grid normalisation divides by dx ((H - 1) // 2) = 0: NaN everywhere, as here
-        assert bool(torch.isnan(ro).all()) and bool(torch.isnan(out).all())
+        assert bool(torch.isnan(r32).all()) and bool(torch.isnan(out).all())
         return
-    # bilinear weights from fp32 coordinates rounded in another order than torch's vectorised CPU
-    # grid_sample: 1.04e-5 drawn for a single sampled row (no averaging over many outputs)
-    assert rel(out, ro) <= 3e-5 and rel(gx, rgx) <= 3e-5
+    # bilinear weights from fp32 coordinates (the reference's, rounded in another order by torch's
+    # vectorised CPU grid_sample): within 1e-5 of the fp64 oracle, or 3 x the reference's own fp32
+    # error where a few edge samples carry the whole output (3.8e-5 drawn for 2 of 44 samples)
+    assert rel(out, r64) <= max(1e-5, 3 * rel(r32, r64)) and rel(gx, rg64) <= max(1e-5, 3 * rel(rg32, rg64))
