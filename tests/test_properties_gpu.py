@@ -390,8 +390,9 @@ def test_optics_elements_vs_oracle(case):
     the field resampler (Addons/Field_Resampler.py:56-118) over drawn shapes, spacings, focal
     lengths, aperture sizes and output grids: the lens within max(4e-6, 2 x the reference's fp32
     error) of the fp64 oracle (its phase pi r^2 / (lambda f) reaches ~10^3 rad here), the aperture
-    bit-exact against the oracle's fp32 mask, the resampler and its gradient within max(1e-5, 3 x
-    the reference's fp32 error) of the oracle's fp64 grid_sample."""
+    bit-exact against the oracle's fp32 mask, the resampler and its gradient per element within the
+    effect of a few ulps of its fp32 sampling coordinates (+ 1e-5 relative) of the oracle's fp64
+    grid_sample."""
     from quantizationawarethzdoe_amd.Addons.Field_Resampler import Field_Resampler
     from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
     from quantizationawarethzdoe_amd.Components.Thin_Lens import Thin_LensElement
@@ -460,7 +461,21 @@ def test_optics_elements_vs_oracle(case):
         # the reference's grid normalisation divides by dx ((H - 1) // 2) = 0: NaN everywhere, as here
         assert bool(torch.isnan(r32).all()) and bool(torch.isnan(out).all())
         return
-    # bilinear weights from fp32 coordinates (the reference's, rounded in another order by torch's
-    # vectorised CPU grid_sample): within 1e-5 of the fp64 oracle, or 3 x the reference's own fp32
-    # error where a few edge samples carry the whole output (3.8e-5 drawn for 2 of 44 samples)
-    assert rel(out, r64) <= max(1e-5, 3 * rel(r32, r64)) and rel(gx, rg64) <= max(1e-5, 3 * rel(rg32, rg64))
+    # The sampling coordinates are fp32: the output grid linspace(-(n-1)//2, (n-1)//2, n) * d_out is
+    # formed as torch's CUDA kernel forms it (start + step i from either end), torch's CPU kernel
+    # (the oracle) in 8-wide vector chunks -- the same values up to an ulp or two of the grid value,
+    # and -34 + step * 34 style sums turn that into ~1e-5 of a pixel.  A bilinear weight moves by at
+    # most the coordinate error (in pixels), so each output may move by that times the sum of its
+    # taps' magnitudes: 4 ulps of the largest grid value, scaled to input pixels, on each axis.
+    def ulp_pix(n_out, d_out, norm, n_in):
+        lmax = float((n_out - 1) // 2)                      # largest |linspace| value
+        gmax = lmax * abs(d_out) / max(norm, 1e-30)         # ... in normalised grid units
+        e_norm = 4.0 * float(np.spacing(np.float32(max(lmax, 1.0)))) * abs(d_out) / max(norm, 1e-30) \
+            + 4.0 * float(np.spacing(np.float32(max(gmax, 1.0))))
+        return e_norm * (n_in - 1) / 2.0                    # in input pixels
+
+    dw = ulp_pix(Ho, dxo, float(np.float32(dx)) * ((H - 1) // 2), H) + ulp_pix(Wo, dyo, float(np.float32(dy)) * ((W - 1) // 2), W)
+    bound = dw * 4 * float(x.abs().max()) + 1e-5 * r64.abs()
+    assert bool(((out.detach().cpu().to(torch.complex128) - r64).abs() <= bound).all()), float(dw)
+    gbound = dw * 4 * float(gout.abs().sum()) + 1e-5 * rg64.abs()
+    assert bool(((gx.detach().cpu().to(torch.complex128) - rg64).abs() <= gbound).all())
