@@ -50,12 +50,13 @@ extern "C" {
 typedef void* thz_stream_t; /* hipStream_t */
 
 /* ABI of this header.  Bumped whenever a descriptor struct changes layout (round 2 appended
- * rng / rng_stream to thz_doe_desc and thz_quant_desc): a caller compares thz_abi_version()
+ * rng / rng_stream to thz_doe_desc and thz_quant_desc; 4 added thz_asm_transfer_function and
+ * thz_rs_kernel, which the bindings require): a caller compares thz_abi_version()
  * with the THZ_ABI_VERSION it was compiled against before its first call, since a shorter
  * struct from an older header would make the library read past it.  Descriptors are plain C
  * structs: zero-initialise them (memset / `= {0}` / ctypes defaults) so fields a caller does not
  * know about stay 0 (no noise buffer and no device generator means no noise). */
-#define THZ_ABI_VERSION 3
+#define THZ_ABI_VERSION 4
 
 /* Library identity. */
 const char* thz_version(void);
@@ -99,6 +100,13 @@ int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out, void* work
 /* Plan facts for diagnostics / bench byte counts: number of spectral columns the kernels
  * keep (|m_y| <= J; ncols = 2J+1, or Pw when nothing is cut) and z-planes per column pass. */
 int thz_asm_band(const thz_asm_desc* d, int* ncols, int* z_chunk);
+/* The transfer function the ASM kernels apply on the fly, materialised for inspection:
+ * ASM_prop.create_kernel (Props/ASM_Prop.py:212-311; used by visualize_kernel, :198-210).
+ * out [C, Ph, Pw] complex64 (device) on the CENTRED frequency grid of the padded plane
+ * (row i <-> Kx = 2 pi ((i - Ph/2) / Ph) / dx, :141-145, 244-245), H = exp(i z sqrt(k^2 - K^2))
+ * with the evanescent cut (:262) and the desc's band limit (:264-309), z = d->z[0].
+ * Uses C, H, W, pad_h, pad_w, bandlimit, dx, dy, wavelengths, z of the descriptor. */
+int thz_asm_transfer_function(const thz_asm_desc* d, void* out, thz_stream_t stream);
 
 /*
  * Chirp-z (Bluestein) Rayleigh-Sommerfeld propagation with output zoom,
@@ -149,6 +157,13 @@ typedef struct thz_rsc_desc {
 int thz_rsc_workspace_size(const thz_rsc_desc* d, size_t* bytes);
 int thz_rsc_forward(const thz_rsc_desc* d, const void* in, void* out, void* workspace, size_t workspace_bytes,
                     thz_stream_t stream);
+
+/* The Rayleigh-Sommerfeld kernel exp(i k r) z / (2 pi r^2) (1/r - i k), r = sqrt(x^2 + y^2 + z^2),
+ * k = 2 pi / lambda_c, on n mesh points: CZT_prop.RS_kernel (Props/CZT_Prop.py:44-57) and the
+ * spatial kernel of RSC_prop.create_kernel (Props/RSC_Prop.py:144-167).  x[n], y[n] device
+ * floats (the meshes), wavelengths[C] host floats; out [C][n] complex64 (device). */
+int thz_rs_kernel(const float* x, const float* y, int n, float z, const float* wavelengths, int C, void* out,
+                  thz_stream_t stream);
 
 /*
  * DOE modulation, DOELayer.modulate (Components/QuantizedDOE.py:92-126):

@@ -7,6 +7,8 @@ the half field size is an error (the reference fails there with an unbound local
 """
 from __future__ import annotations
 
+import types
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -37,19 +39,59 @@ class ApertureElement(nn.Module):
             return float(_f32(size / 2))
         return float(full / _f32(2))
 
+    def _mask(self, kind, field, **size):
+        dx, dy = field.spacing_host
+        ones = torch.ones((1, 1, field.height, field.width), dtype=torch.complex64, device=field.device)
+        return _optics.aperture(ones, kind, dx, dy, **size).real.to(torch.int64)
+
+    def _circ_radius(self, field, radius):
+        dx, dy = field.spacing_host
+        if radius is None:
+            raise TypeError("circ aperture needs a radius (the reference fails on torch.tensor(None))")
+        if not _f32(radius) < min(_f32(dx) * _f32(field.height), _f32(dy) * _f32(field.width)) / _f32(2):
+            raise ValueError('The radius should not larger than the physical length of E-field ')
+        return radius
+
+    def add_circ_aperture_to_field(self, input_field: ElectricField, radius=None) -> torch.Tensor:
+        """The circular mask [1, 1, H, W] (int64: 1 where sqrt(X^2 + Y^2) <= r), Components/Aperture.py:
+        44-73, from the HIP aperture kernel applied to a unit field."""
+        return self._mask(_lib.APERTURE_CIRC, input_field, radius=self._circ_radius(input_field, radius))
+
+    def add_rect_aperture_to_field(self, input_field: ElectricField, rect_width=None, rect_height=None) -> torch.Tensor:
+        """The rectangular mask [1, 1, H, W] (int64), Components/Aperture.py:75-102: sizes default to
+        half the field and are clipped to it."""
+        dx, dy = input_field.spacing_host
+        return self._mask(_lib.APERTURE_RECT, input_field,
+                          half_w=self._rect_half(rect_width, dx, input_field.width),
+                          half_h=self._rect_half(rect_height, dy, input_field.height))
+
+    @property
+    def aperture(self):
+        """The mask of the last forward (Components/Aperture.py:112-123 stores it as ``self.aperture``),
+        formed on first read instead of on every call."""
+        src = self.__dict__.get("_aperture_src")
+        if src is None:
+            raise AttributeError("'ApertureElement' has no aperture before its first forward")
+        kind, field = src  # the last input's geometry (not its data)
+        if kind == 'circ':
+            return self.add_circ_aperture_to_field(field, radius=self.aperture_size)
+        if kind == 'rect':
+            return self.add_rect_aperture_to_field(field, rect_height=self.aperture_size, rect_width=self.aperture_size)
+        return torch.ones(field.shape, dtype=field.dtype, device=field.device)
+
     def forward(self, field: ElectricField) -> ElectricField:
         dx, dy = field.spacing_host
         H, W = field.height, field.width
+        self.__dict__["_aperture_src"] = (self.aperture_type, types.SimpleNamespace(
+            spacing_host=field.spacing_host, height=H, width=W, shape=tuple(field.shape), dtype=field.data.dtype,
+            device=field.device))
         if self.aperture_type == 'rect':
             out = _optics.aperture(field.data, _lib.APERTURE_RECT, dx, dy,
                                    half_w=self._rect_half(self.aperture_size, dx, W),
                                    half_h=self._rect_half(self.aperture_size, dy, H))
         elif self.aperture_type == 'circ':
-            if self.aperture_size is None:
-                raise TypeError("circ aperture needs a radius (the reference fails on torch.tensor(None))")
-            if not _f32(self.aperture_size) < min(_f32(dx) * _f32(H), _f32(dy) * _f32(W)) / _f32(2):
-                raise ValueError('The radius should not larger than the physical length of E-field ')
-            out = _optics.aperture(field.data, _lib.APERTURE_CIRC, dx, dy, radius=self.aperture_size)
+            out = _optics.aperture(field.data, _lib.APERTURE_CIRC, dx, dy,
+                                   radius=self._circ_radius(field, self.aperture_size))
         elif self.aperture_type is None:
             out = field.data
         else:

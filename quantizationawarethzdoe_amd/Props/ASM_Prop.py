@@ -104,6 +104,77 @@ class ASM_prop(nn.Module):
         self._z = z
         self._zh = _z_host(z)
 
+    # -- frequency grid and transfer function, for inspection (Props/ASM_Prop.py:138-311) ------
+    def create_frequency_grid(self, H, W):
+        """Normalised centred frequency grids (i - H//2)/H and (j - W//2)/W, meshgrid 'ij'
+        (Props/ASM_Prop.py:138-145), as the ``Kx`` / ``Ky`` buffers.  The kernels form the same
+        values per element and never read these."""
+        with torch.no_grad():
+            fx = (torch.arange(H, dtype=torch.float32) - (H // 2)) / H
+            fy = (torch.arange(W, dtype=torch.float32) - (W // 2)) / W
+            self.Kx, self.Ky = torch.meshgrid(fx, fy, indexing="ij")
+        self._grid_shape = self._shape
+
+    @property
+    def shape(self):
+        return self._shape
+
+    @shape.setter
+    def shape(self, shape):
+        """The padded field shape of the last call (Props/ASM_Prop.py:151-167).  The reference
+        rebuilds Kx / Ky whenever (H, W) changes; here they are built when first read after such a
+        change (a P = 8192 grid is 512 MB of host memory that no kernel uses)."""
+        self._shape = shape
+
+    def _grid(self):
+        shp = self._shape
+        if shp is not None and (getattr(self, "_grid_shape", None) is None
+                                or tuple(self._grid_shape[-2:]) != tuple(shp[-2:])):
+            self.create_frequency_grid(int(shp[-2]), int(shp[-1]))
+
+    @property
+    def Kx(self):
+        self._grid()
+        return self._Kx
+
+    @Kx.setter
+    def Kx(self, Kx):
+        self.register_buffer("_Kx", Kx)
+
+    @property
+    def Ky(self):
+        self._grid()
+        return self._Ky
+
+    @Ky.setter
+    def Ky(self, Ky):
+        self.register_buffer("_Ky", Ky)
+
+    def create_kernel(self, field: ElectricField) -> torch.Tensor:
+        """The band-limited transfer function [1, C, Ph, Pw] on the centred grid of the padded
+        plane (Props/ASM_Prop.py:212-311), with the once-per-instance critical-distance print.
+        The propagators never build it (they evaluate H per element); this materialises the same
+        values with the HIP kernel thz_asm_transfer_function for inspection."""
+        B, C, H, W = field.shape
+        ph, pw = self.compute_padding(H, W, return_size_of_padding=True)
+        self.shape = torch.Size([B, C, H + 2 * ph, W + 2 * pw])
+        sp, wl = field.spacing_host, field.wavelengths_host
+        bl = self._bandlimit_code()
+        self._zc_diagnostic(H + 2 * ph, sp[0], wl, self._zh[0])
+        return _prop.asm_transfer_function(wl, sp, self._zh[0], H, W, ph, pw, bl, field.device)
+
+    def visualize_kernel(self, field: ElectricField):
+        """Amplitude and phase of create_kernel(field) (Props/ASM_Prop.py:198-210)."""
+        import matplotlib.pyplot as plt
+        kernel = self.create_kernel(field=field)
+        plt.subplot(121)
+        plt.imshow(kernel.abs().cpu().squeeze(), vmin=0)
+        plt.title("Amplitude")
+        plt.subplot(122)
+        plt.imshow(kernel.angle().cpu().squeeze())
+        plt.title("Phase")
+        plt.tight_layout()
+
     def compute_padding(self, H, W, return_size_of_padding=False):
         """Props/ASM_Prop.py:119-136."""
         if not self.do_padding:
@@ -145,6 +216,7 @@ class ASM_prop(nn.Module):
         data = pend.field if pend is not None else field.data
         B, C, H, W = data.shape
         ph, pw = self.compute_padding(H, W, return_size_of_padding=True)
+        self.shape = torch.Size([B, C, H + 2 * ph, W + 2 * pw])
         bl = self._bandlimit_code()
         wl = field.wavelengths_host
         sp = field.spacing_host

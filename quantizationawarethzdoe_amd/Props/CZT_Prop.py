@@ -51,6 +51,33 @@ class CZT_prop(nn.Module):
         import numpy as np
         return 2 ** (np.ceil(np.log2(x))).astype(int)
 
+    def RS_kernel(self, z, meshx, meshy, wavelengths):
+        """exp(ikr) z / (2 pi r^2) (1/r - ik) on the meshes, [1, C, *mesh] (Props/CZT_Prop.py:44-57),
+        evaluated by the HIP kernel thz_rs_kernel (the same device function the CZT passes apply)."""
+        return _prop.rs_kernel(meshx, meshy, _f(z), [_f(v) for v in torch.as_tensor(wavelengths).reshape(-1)])
+
+    def build_CZT_grid(self, z, wavelengths, InputHeight, InputWidth, InputPixel_dx, InputPixel_dy,
+                       outputHeight, outputWidth, outputPixel_dx, outputPixel_dy):
+        """Input / output meshes (linspace(-N d/2, N d/2, N), meshgrid 'ij'), Dm = lambda z / dx_in
+        and the zoom ranges f1 = x_out[0] + Dm/2, f2 = x_out[-1] + Dm/2 of both axes
+        (Props/CZT_Prop.py:62-118); returns (Inmeshx, Inmeshy, Outmeshx, Outmeshy, Dm, fx_1, fx_2,
+        fy_1, fy_2) with Dm and the f's shaped [1, C, 1, 1].  The kernels form these per element
+        (thz_czt.hip); this is the reference's grid API for callers that inspect it."""
+        dev = self.device
+
+        def grid(n, d):
+            e = torch.as_tensor(n * d, dtype=torch.float32) / 2
+            return torch.linspace(float(-e), float(e), int(n), device=dev)
+
+        x_in, y_in = grid(InputHeight, InputPixel_dx), grid(InputWidth, InputPixel_dy)
+        x_out, y_out = grid(outputHeight, outputPixel_dx), grid(outputWidth, outputPixel_dy)
+        Inmeshx, Inmeshy = torch.meshgrid(x_in, y_in, indexing="ij")
+        Outmeshx, Outmeshy = torch.meshgrid(x_out, y_out, indexing="ij")
+        lam = torch.as_tensor(wavelengths, device=dev).reshape(1, -1, 1, 1)
+        Dm = lam * torch.as_tensor(z, device=dev) / torch.as_tensor(InputPixel_dx, device=dev)
+        return (Inmeshx, Inmeshy, Outmeshx, Outmeshy, Dm, x_out[0] + Dm / 2, x_out[-1] + Dm / 2,
+                y_out[0] + Dm / 2, y_out[-1] + Dm / 2)
+
     def forward(self, field: ElectricField, outputHeight=None, outputWidth=None, outputPixel_dx=None,
                 outputPixel_dy=None) -> ElectricField:
         sp = field.spacing_host

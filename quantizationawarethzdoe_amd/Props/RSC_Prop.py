@@ -76,6 +76,30 @@ class RSC_prop(nn.Module):
             print("The propagation distance should be larger than minimum propagation distance to keep "
                   "simulation accurate!")
 
+    def create_spatial_grid(self, H, W, dx, dy):
+        """linspace(-N dx/2, N dx/2, N) on both axes WITH dx (Props/RSC_Prop.py:79-87, the
+        reference's y grid uses dx too), meshgrid 'ij', on the module's device."""
+        def grid(n):
+            e = (np.float32(-n) * np.float32(_f(dx))) / np.float32(2), (np.float32(n) * np.float32(_f(dx))) / np.float32(2)
+            return torch.linspace(float(e[0]), float(e[1]), int(n))
+        meshx, meshy = torch.meshgrid(grid(H), grid(W), indexing="ij")
+        return meshx.to(device=self.device), meshy.to(device=self.device)
+
+    def create_kernel(self, field: ElectricField) -> torch.Tensor:
+        """The spatial RS kernel exp(ikr) z/(2 pi r^2)(1/r - ik) on the padded grid, [1, C, Ph, Pw]
+        (Props/RSC_Prop.py:129-167), with the once-per-instance minimum-distance print.  The
+        convolution kernels take FFT2 of the same values in-kernel; this materialises them with
+        thz_rs_kernel for inspection and sets ``meshx`` / ``meshy`` as the reference does."""
+        B, C, H, W = field.shape
+        Ph, Pw = self.compute_padding(H, W)
+        sp, wl = field.spacing_host, field.wavelengths_host
+        self.meshx, self.meshy = self.create_spatial_grid(Ph, Pw, sp[0], sp[1])
+        if self.check_Zc:
+            self.shape = field.shape
+            self.check_RS_minimum_z(1, sp[0], sp[1], min(wl), Ph=Ph)
+            self.check_Zc = False
+        return _prop.rs_kernel(self.meshx, self.meshy, self._zh, wl)
+
     def forward(self, field: ElectricField) -> ElectricField:
         data = field.data
         B, C, H, W = self.shape = data.shape

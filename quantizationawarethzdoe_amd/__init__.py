@@ -8,7 +8,7 @@ the hand-written gfx950 kernels of ``libthzdoe.so`` (``csrc/``) via ``_lib``.
 import importlib
 import sys
 
-__version__ = "0.3.0"
+__version__ = "0.4.0"
 
 _ALIASES = ("DataType", "Props", "Components", "LightSource", "utils", "Addons", "VisTools")
 

@@ -20,7 +20,7 @@ THZ_E_WORKSPACE = 3
 THZ_E_HIP = 4
 THZ_MAX_WAVELENGTHS = 64
 THZ_MAX_Z = 256
-THZ_ABI_VERSION = 3  # include/thzdoe.h: the descriptor layouts below
+THZ_ABI_VERSION = 4  # include/thzdoe.h: the descriptor layouts below
 
 BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 
@@ -28,7 +28,7 @@ BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 EXPORTED = [
     "thz_version", "thz_last_error", "thz_abi_version",
     "thz_asm_workspace_size", "thz_asm_forward", "thz_asm_band", "thz_asm_forward_modulated",
-    "thz_asm_forward_loss", "thz_asm_adjoint_loss",
+    "thz_asm_forward_loss", "thz_asm_adjoint_loss", "thz_asm_transfer_function", "thz_rs_kernel",
     "thz_czt_workspace_size", "thz_czt_forward",
     "thz_rsc_workspace_size", "thz_rsc_forward",
     "thz_doe_modulate_forward", "thz_doe_modulate_backward", "thz_quant_forward", "thz_quant_backward",
@@ -204,6 +204,8 @@ def _declare(lib):
     lib.thz_gaussian_beam.argtypes = [ctypes.POINTER(GaussDesc), c_void_p, c_void_p]
     lib.thz_thin_lens.argtypes = [ctypes.POINTER(LensDesc), c_void_p, c_void_p, c_void_p]
     lib.thz_aperture.argtypes = [ctypes.POINTER(ApertureDesc), c_void_p, c_void_p, c_void_p]
+    lib.thz_asm_transfer_function.argtypes = [ctypes.POINTER(AsmDesc), c_void_p, c_void_p]
+    lib.thz_rs_kernel.argtypes = [c_void_p, c_void_p, c_int, ctypes.c_float, c_void_p, c_int, c_void_p, c_void_p]
     lib.thz_intensity_mse_workspace_size.argtypes = [ctypes.POINTER(LossDesc)]
     lib.thz_intensity_mse_forward.argtypes = [ctypes.POINTER(LossDesc), c_void_p, c_void_p, c_void_p, c_void_p,
                                               c_void_p]

@@ -1404,6 +1404,44 @@ extern "C" int thz_asm_forward(const thz_asm_desc* d, const void* in, void* out,
   return asm_forward_impl(d, nullptr, nullptr, nullptr, nullptr, in, out, workspace, workspace_bytes, stream);
 }
 
+namespace thz {
+// ASM_prop.create_kernel (Props/ASM_Prop.py:212-311): H of one z on the CENTRED grid of the padded
+// plane, [C][Ph][Pw], the row i / column j at spectral index m = i - Ph/2 (:141-145).  The same
+// fp32 scalars, masks and phase as the propagation kernels (tf_scalars / tf_value), so the table
+// is exactly the transfer function they apply on the fly; only inspection reads it
+// (ASM_prop.visualize_kernel).
+__global__ void __launch_bounds__(256) asm_tf_export(float2* __restrict__ out, AsmArgs a) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, i = blockIdx.y, c = blockIdx.z;
+  if (j >= a.Pw) return;
+  const TfScalars s = tf_scalars(a, a.lam[c], a.zv[0]);
+  const float Kx = kfreq(i - a.Ph / 2, a.Ph, a.dx), Ky = kfreq(j - a.Pw / 2, a.Pw, a.dy);
+  out[((size_t)c * a.Ph + i) * a.Pw + j] = tf_value(a, s, Kx, Ky);
+}
+}  // namespace thz
+
+extern "C" int thz_asm_transfer_function(const thz_asm_desc* d, void* out, thz_stream_t stream) {
+  int e = validate(d);
+  if (e) return e;
+  if (!out) return fail(THZ_E_ARG, "null output pointer");
+  AsmGeom g;
+  geometry(d, &g);
+  AsmArgs a{};
+  a.C = d->C;
+  a.Ph = g.Ph;
+  a.Pw = g.Pw;
+  a.bl = d->bandlimit;
+  a.dx = d->dx;
+  a.dy = d->dy;
+  for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
+  a.zv[0] = d->z[0];
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("asm_tf_export", s);
+  hipLaunchKernelGGL(asm_tf_export, dim3((g.Pw + 255) / 256, g.Ph, d->C), dim3(256), 0, s, (float2*)out, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
 extern "C" int thz_asm_forward_modulated(const thz_asm_desc* d, const thz_doe_desc* m, const void* field,
                                          const float* height, const float* noise, float* height_full, void* out,
                                          void* workspace, size_t workspace_bytes, thz_stream_t stream) {

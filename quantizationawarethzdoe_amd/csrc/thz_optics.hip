@@ -394,6 +394,44 @@ extern "C" int thz_thin_lens(const thz_lens_desc* d, const void* in, void* out, 
   return THZ_OK;
 }
 
+// CZT_prop.RS_kernel (Props/CZT_Prop.py:44-57) and RSC_prop.create_kernel (Props/RSC_Prop.py:
+// 157-160): exp(i k r) z / (2 pi r^2) (1/r - i k), r = sqrt(x^2 + y^2 + z^2), on n mesh points per
+// wavelength.  The phase k r is formed as (k |z|) mod 2 pi + k rho^2 / (r + |z|) with k |z| in
+// double (rs_kernel), as in the CZT passes.
+struct RsExportArgs {
+  int n, C;
+  float z;
+  float lam[THZ_MAX_WAVELENGTHS];
+};
+__global__ void __launch_bounds__(EW_THREADS) rs_kernel_export(const float* __restrict__ x, const float* __restrict__ y,
+                                                               float2* __restrict__ out, RsExportArgs a) {
+  const int c = blockIdx.y;
+  const float lam = a.lam[c];
+  const RsPhase ph = rs_phase(lam, a.z);
+  const float k = 6.283185307179586f / lam;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += gridDim.x * blockDim.x)
+    out[(size_t)c * a.n + i] = rs_kernel(x[i], y[i], a.z, k, ph);
+}
+
+extern "C" int thz_rs_kernel(const float* x, const float* y, int n, float z, const float* wavelengths, int C,
+                             void* out, thz_stream_t stream) {
+  if (!x || !y || !out || !wavelengths || n < 0 || C < 1) return fail(THZ_E_ARG, "bad RS-kernel arguments");
+  if (C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", C, THZ_MAX_WAVELENGTHS);
+  if (n == 0) return THZ_OK;
+  RsExportArgs a{};
+  a.n = n;
+  a.C = C;
+  a.z = z;
+  for (int c = 0; c < C; ++c) a.lam[c] = wavelengths[c];
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("rs_kernel_export", s);
+  const int blocks = std::min((n + EW_THREADS - 1) / EW_THREADS, 4096);
+  hipLaunchKernelGGL(rs_kernel_export, dim3(blocks, C), dim3(EW_THREADS), 0, s, x, y, (float2*)out, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
 extern "C" int thz_aperture(const thz_aperture_desc* d, const void* in, void* out, thz_stream_t stream) {
   if (!d || !in || !out || d->BC < 1 || d->H < 1 || d->W < 1) return fail(THZ_E_ARG, "bad aperture arguments");
   if (d->kind != THZ_APERTURE_RECT && d->kind != THZ_APERTURE_CIRC)

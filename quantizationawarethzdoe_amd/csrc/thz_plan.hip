@@ -163,6 +163,6 @@ extern "C" int thz_timing_read(const char* kernel, double* total_ms, long* launc
   return THZ_OK;
 }
 
-extern "C" const char* thz_version(void) { return "thzdoe 0.3.0 gfx950"; }
+extern "C" const char* thz_version(void) { return "thzdoe 0.4.0 gfx950"; }
 extern "C" int thz_abi_version(void) { return THZ_ABI_VERSION; }
 extern "C" const char* thz_last_error(void) { return thz::g_err.c_str(); }

@@ -168,6 +168,41 @@ class _AsmFunction(torch.autograd.Function):
         return gin, None, None, None, None, None, None, None, None
 
 
+def asm_transfer_function(wavelengths, spacing, z, H, W, pad_h, pad_w, bandlimit, device):
+    """ASM_prop.create_kernel's table (Props/ASM_Prop.py:212-311): [1, C, Ph, Pw] complex64 on the
+    centred frequency grid, computed by the HIP kernel the propagators evaluate on the fly."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError(f"ASM transfer function: the MI355X path needs a ROCm device (got {dev}); "
+                           "this framework has no CPU compute path")
+    bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
+    d = _asm_desc(1, len(wavelengths), int(H), int(W), int(pad_h), int(pad_w), True, bl, wavelengths, spacing,
+                  [float(z)], False)
+    out = torch.empty((1, len(wavelengths), H + 2 * pad_h, W + 2 * pad_w), dtype=torch.complex64, device=dev)
+    with torch.cuda.device(dev):
+        _lib.check(_lib.lib().thz_asm_transfer_function(ctypes.byref(d), ctypes.c_void_p(out.data_ptr()),
+                                                         _stream_handle()))
+    return out
+
+
+def rs_kernel(meshx, meshy, z, wavelengths):
+    """exp(ikr) z/(2 pi r^2) (1/r - ik) on the meshes for each wavelength (Props/CZT_Prop.py:44-57,
+    Props/RSC_Prop.py:157-160): [1, C, *mesh.shape] complex64 from the HIP kernel thz_rs_kernel."""
+    _require_device(meshx, "RS kernel")
+    mx, my = torch.broadcast_tensors(meshx, meshy)
+    shape = tuple(mx.shape)
+    mx = mx.detach().to(torch.float32).contiguous().reshape(-1)
+    my = my.detach().to(device=mx.device, dtype=torch.float32).contiguous().reshape(-1)
+    wl = [float(v) for v in wavelengths]
+    arr = _lib.float_array(wl)
+    out = torch.empty((1, len(wl)) + shape, dtype=torch.complex64, device=mx.device)
+    with torch.cuda.device(mx.device):
+        _lib.check(_lib.lib().thz_rs_kernel(ctypes.c_void_p(mx.data_ptr()), ctypes.c_void_p(my.data_ptr()),
+                                            int(mx.numel()), ctypes.c_float(float(z)), ctypes.cast(arr, ctypes.c_void_p), len(wl),
+                                            ctypes.c_void_p(out.data_ptr()), _stream_handle()))
+    return out
+
+
 def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", z_chunk=0):
     """Differentiable ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo] (HIP kernels)."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit

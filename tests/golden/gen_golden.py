@@ -681,6 +681,103 @@ def gen_save(manifest):
     print("save", len(data), "bytes")
 
 
+def gen_introspect(manifest):
+    """The reference's inspection API on small cases (introspect_golden.npz): ASM_prop.create_kernel
+    and its Kx / Ky grid (Props/ASM_Prop.py:138-311), RSC_prop.create_kernel and its meshes
+    (Props/RSC_Prop.py:79-167), CZT_prop.build_CZT_grid / RS_kernel (Props/CZT_Prop.py:44-118), and
+    ApertureElement.add_*_aperture_to_field (Components/Aperture.py:44-102); kernels in fp32 as
+    shipped and in fp64 (the SURVEY §8(c) procedure)."""
+    AP = ref.import_module("Components.Aperture")
+    arrays, cases = {}, []
+    asm_cases = [dict(name="tf_exact_s1", f=[300], H=64, W=64, dx=0.5, dy=0.5, z=0.05, s=1, bl=True, t="exact"),
+                 dict(name="tf_approx_s15_2wl", f=[280, 320], H=48, W=80, dx=0.5, dy=0.75, z=0.2, s=1.5, bl=True,
+                      t="approx"),
+                 dict(name="tf_nobl_negz", f=[300], H=50, W=50, dx=1.0, dy=1.0, z=-0.1, s=2, bl=False, t="exact"),
+                 dict(name="tf_nopad", f=[300], H=40, W=40, dx=1.0, dy=1.0, z=0.3, s=1, bl=True, t="exact",
+                      do_padding=False)]
+    for c in asm_cases:
+        wl = [C0 / (g * 1e9) for g in c["f"]]
+        x = np.ones((1, len(wl), c["H"], c["W"]), np.complex64)
+        for f64 in (False, True):
+            with default_dtype(torch.float64 if f64 else torch.float32):
+                field = make_field(x, wl_arg(wl), [c["dx"] * MM, c["dy"] * MM], f64)
+                prop = ref.ASM.ASM_prop(z_distance=c["z"], do_padding=c.get("do_padding", True), padding_scale=c["s"],
+                                        bandlimit_kernel=c["bl"], bandlimit_type=c["t"], device="cpu")
+                H, txt = quiet(prop.create_kernel, field)
+            tag = "64" if f64 else "32"
+            arrays[f"{c['name']}__H{tag}"] = H.detach().numpy()
+            if not f64:
+                arrays[f"{c['name']}__Kx"] = prop.Kx.numpy()
+                arrays[f"{c['name']}__Ky"] = prop.Ky.numpy()
+                c["print"] = txt
+        cases.append(c)
+    # RSC spatial kernel (dx on both axes) and its meshes
+    rc = dict(name="rsc_k", f=[300, 330], H=32, W=32, dx=1.0, dy=1.0, z=0.3)
+    wl = [C0 / (g * 1e9) for g in rc["f"]]
+    x = np.ones((1, 2, rc["H"], rc["W"]), np.complex64)
+    for f64 in (False, True):
+        with default_dtype(torch.float64 if f64 else torch.float32):
+            field = make_field(x, wl_arg(wl), [rc["dx"] * MM, rc["dy"] * MM], f64)
+            prop = ref.RSC.RSC_prop(z_distance=rc["z"], device="cpu")
+            prop.shape = field.data.shape
+            K, txt = quiet(prop.create_kernel, field)
+        tag = "64" if f64 else "32"
+        arrays[f"rsc_k__K{tag}"] = K.detach().numpy()
+        if not f64:
+            arrays["rsc_k__meshx"] = prop.meshx.numpy()
+            arrays["rsc_k__meshy"] = prop.meshy.numpy()
+            rc["print"] = txt
+    # the same formula in fp64 on the fp32 meshes and the fp32-rounded z (CZT_prop.RS_kernel is RSC's
+    # kernel expression, Props/CZT_Prop.py:44-57 vs Props/RSC_Prop.py:157-160): isolates the kernel
+    # from the grid and z rounding
+    with default_dtype(torch.float64):
+        cz = ref.CZT.CZT_prop(z_distance=rc["z"], device="cpu")
+        arrays["rsc_k__K64on32"] = cz.RS_kernel(torch.tensor(rc["z"], dtype=torch.float32).double(),
+                                                torch.from_numpy(arrays["rsc_k__meshx"]).double(),
+                                                torch.from_numpy(arrays["rsc_k__meshy"]).double(),
+                                                torch.tensor(wl, dtype=torch.float32).double()).numpy()
+    cases.append(rc)
+    # CZT grid and RS kernels (the input and output planes of forward, :236-238)
+    cc = dict(name="czt_grid", f=[220, 330], H=40, W=40, dx=0.5, dy=0.5, outH=16, outW=16, odx=0.25, ody=0.25,
+              z=0.5)
+    wl = [C0 / (g * 1e9) for g in cc["f"]]
+    for f64 in (False, True):
+        with default_dtype(torch.float64 if f64 else torch.float32):
+            field = make_field(np.ones((1, 2, cc["H"], cc["W"]), np.complex64), wl_arg(wl),
+                               [cc["dx"] * MM, cc["dy"] * MM], f64)
+            prop = ref.CZT.CZT_prop(z_distance=cc["z"], device="cpu")
+            g = prop.build_CZT_grid(prop._z, field.wavelengths, cc["H"], cc["W"], field.spacing[0], field.spacing[1],
+                                    cc["outH"], cc["outW"], cc["odx"] * MM, cc["ody"] * MM)
+            F = prop.RS_kernel(prop._z, g[0], g[1], field.wavelengths)
+            F0 = prop.RS_kernel(prop._z, g[2], g[3], field.wavelengths)
+        tag = "64" if f64 else "32"
+        arrays[f"czt_grid__F{tag}"] = F.numpy()
+        arrays[f"czt_grid__F0{tag}"] = F0.numpy()
+        if not f64:
+            for k, v in zip(("Inmeshx", "Inmeshy", "Outmeshx", "Outmeshy", "Dm", "fx_1", "fx_2", "fy_1", "fy_2"), g):
+                arrays[f"czt_grid__{k}"] = v.numpy()
+        else:  # the fp64 kernel on the fp32 meshes
+            m32 = [torch.from_numpy(arrays[f"czt_grid__{k}"]).double()
+                   for k in ("Inmeshx", "Inmeshy", "Outmeshx", "Outmeshy")]
+            with default_dtype(torch.float64):
+                z32 = torch.tensor(cc["z"], dtype=torch.float32).double()
+                arrays["czt_grid__F64on32"] = prop.RS_kernel(z32, m32[0], m32[1], field.wavelengths).numpy()
+                arrays["czt_grid__F064on32"] = prop.RS_kernel(z32, m32[2], m32[3], field.wavelengths).numpy()
+    cases.append(cc)
+    # aperture masks
+    x = np.ones((1, 1, 30, 44), np.complex64)
+    field = make_field(x, C0 / 300e9, [0.5 * MM, 0.7 * MM], False)
+    el = AP.ApertureElement(aperture_type="circ", aperture_size=0.006)
+    arrays["ap__circ"] = el.add_circ_aperture_to_field(field, radius=0.006).numpy()
+    arrays["ap__rect_default"] = el.add_rect_aperture_to_field(field).numpy()
+    arrays["ap__rect_wh"] = el.add_rect_aperture_to_field(field, rect_width=0.012, rect_height=0.5).numpy()
+    cases.append(dict(name="ap", H=30, W=44, dx=0.5 * MM, dy=0.7 * MM, f=[300], circ=0.006, rect_w=0.012,
+                      rect_h=0.5))
+    np.savez_compressed(os.path.join(HERE, "introspect_golden.npz"), **arrays)
+    manifest["introspect"] = cases
+    print("introspect", len(cases))
+
+
 def main():
     path = os.path.join(HERE, "manifest.json")
     if "--only" in sys.argv:
@@ -688,7 +785,7 @@ def main():
         with open(path) as fh:
             manifest = json.load(fh)
         {"doe_layers": gen_doe_layers, "optics": gen_optics, "qat": gen_qat, "donn": gen_donn,
-         "addons": gen_addons, "vrs": gen_vrs, "save": gen_save}[which](manifest)
+         "addons": gen_addons, "vrs": gen_vrs, "save": gen_save, "introspect": gen_introspect}[which](manifest)
     else:
         manifest = {"generator": "tests/golden/gen_golden.py", "torch": torch.__version__,
                     "asm": [], "czt": [], "rsc": [], "doe": []}
@@ -703,6 +800,7 @@ def main():
         gen_donn(manifest)
         gen_addons(manifest)
         gen_save(manifest)
+        gen_introspect(manifest)
     with open(path, "w") as fh:
         json.dump(manifest, fh, indent=1, default=float)
 

@@ -51,6 +51,18 @@ int main(void) {
   EXPECT(thz_asm_forward(&a, NULL, NULL, NULL, 0, NULL) != THZ_OK, "asm forward null data");
   char dummy[64];
   EXPECT(thz_asm_forward(&a, dummy, dummy, dummy, 8, NULL) == THZ_E_WORKSPACE, "asm workspace too small");
+  /* inspection entries: rejections before any launch */
+  EXPECT(thz_asm_transfer_function(NULL, dummy, NULL) != THZ_OK, "transfer function null descriptor");
+  EXPECT(thz_asm_transfer_function(&a, NULL, NULL) == THZ_E_ARG, "transfer function null output");
+  b = a; b.W = -1;
+  EXPECT(thz_asm_transfer_function(&b, dummy, NULL) != THZ_OK, "transfer function bad shape");
+  EXPECT(thz_rs_kernel(NULL, (const float*)dummy, 4, 0.1f, wl, 2, dummy, NULL) == THZ_E_ARG, "rs kernel null mesh");
+  EXPECT(thz_rs_kernel((const float*)dummy, (const float*)dummy, 4, 0.1f, wl, 0, dummy, NULL) == THZ_E_ARG,
+         "rs kernel no wavelength");
+  EXPECT(thz_rs_kernel((const float*)dummy, (const float*)dummy, 4, 0.1f, wl, THZ_MAX_WAVELENGTHS + 1, dummy, NULL) ==
+             THZ_E_UNSUPPORTED, "rs kernel too many wavelengths");
+  EXPECT(thz_rs_kernel((const float*)dummy, (const float*)dummy, 0, 0.1f, wl, 2, dummy, NULL) == THZ_OK,
+         "rs kernel on an empty mesh is a no-op");
 
   /* fused entries: shape agreement is checked before anything runs */
   thz_doe_desc m;

@@ -368,3 +368,50 @@ def test_e2e_designed_doe_oracle_matches_reference(name):
     assert abs(float(loss) - float(A[f"{name}__loss32"])) <= 1e-5 * float(A[f"{name}__loss32"])
     loss.backward()
     assert rel_l2(h.grad.numpy(), A[f"{name}__grad32"]) <= 1e-4
+
+
+def _introspect():
+    import json
+    import os
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    with np.load(os.path.join(here, "introspect_golden.npz"), allow_pickle=False) as z:
+        A = {k: z[k] for k in z.files}
+    with open(os.path.join(here, "manifest.json")) as fh:
+        return A, {c["name"]: c for c in json.load(fh)["introspect"]}
+
+
+@pytest.mark.parametrize("name", ["tf_exact_s1", "tf_approx_s15_2wl", "tf_nobl_negz", "tf_nopad"])
+def test_asm_transfer_function_oracle_matches_reference_create_kernel(name):
+    """oracle.asm_transfer_function == the reference's ASM_prop.create_kernel (fp32 as shipped, and in
+    fp64 by the SURVEY §8(c) procedure), Props/ASM_Prop.py:212-311."""
+    A, cases = _introspect()
+    c = cases[name]
+    lam = torch.tensor([2.998e8 / (g * 1e9) for g in c["f"]], dtype=torch.float32)
+    ph, pw, _, _ = orc.asm_padding(c["H"], c["W"], (c["s"], c["s"]), c.get("do_padding", True))
+    dx = torch.tensor(c["dx"] * 1e-3, dtype=torch.float32)
+    dy = torch.tensor(c["dy"] * 1e-3, dtype=torch.float32)
+    for rdt, key in ((torch.float32, "H32"), (torch.float64, "H64")):
+        H = orc.asm_transfer_function(c["H"] + 2 * ph, c["W"] + 2 * pw, lam.to(rdt), dx.to(rdt), dy.to(rdt),
+                                      c["z"], c["bl"], c["t"], rdt=rdt)
+        ref = A[f"{name}__{key}"]
+        assert H.shape == ref.shape
+        assert np.abs(H.numpy() - ref).max() <= (2e-6 if rdt == torch.float32 else 1e-12)
+
+
+def test_rs_kernel_oracle_matches_reference():
+    """oracle._rs_kernel on the reference's own (fp32) meshes == CZT_prop.RS_kernel and
+    RSC_prop.create_kernel (Props/CZT_Prop.py:44-57, Props/RSC_Prop.py:157-160), in fp32 and with the
+    reference's kernel expression evaluated in fp64 on the same meshes."""
+    A, cases = _introspect()
+    for pre, key_x, key_y, ks, c in (("czt_grid", "Inmeshx", "Inmeshy", ("F32", "F64on32"), cases["czt_grid"]),
+                                     ("czt_grid", "Outmeshx", "Outmeshy", ("F032", "F064on32"), cases["czt_grid"]),
+                                     ("rsc_k", "meshx", "meshy", ("K32", "K64on32"), cases["rsc_k"])):
+        lam = torch.tensor([2.998e8 / (g * 1e9) for g in c["f"]], dtype=torch.float32)
+        for rdt, k in zip((torch.float32, torch.float64), ks):
+            mx = torch.from_numpy(A[f"{pre}__{key_x}"]).to(rdt)
+            my = torch.from_numpy(A[f"{pre}__{key_y}"]).to(rdt)
+            F = orc._rs_kernel(torch.tensor(c["z"], dtype=torch.float32).to(rdt), mx, my, lam.to(rdt))
+            ref = A[f"{pre}__{k}"]
+            assert F.shape == ref.shape
+            tol = 1e-6 if rdt == torch.float32 else 1e-12
+            assert np.abs(F.numpy() - ref).max() <= tol * np.abs(ref).max(), (pre, k)
