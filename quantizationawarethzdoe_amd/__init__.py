@@ -17,7 +17,7 @@ _MODULES = ("DataType.ElectricField", "Props.ASM_Prop", "Props.CZT_Prop", "Props
             "Components.QuantizedDOE", "Components.Thin_Lens", "Components.Aperture",
             "LightSource.Gaussian_beam", "Addons.Field_Resampler", "Addons.Field_Crop",
             "utils.units", "utils.Visualization_Helper", "utils.Helper_Functions",
-            "VisTools.directions", "VisTools.calc_loss")
+            "VisTools.directions", "VisTools.calc_loss", "VisTools.visualize")
 
 
 def install_reference_aliases():
