@@ -526,6 +526,31 @@ def launch_ranks(args):
     sys.exit(subprocess.call(cmd))
 
 
+def _secondary_watchdog(line, keys, rank, timeout_s):
+    """A timer that, should the secondary measurements outlive ``timeout_s``, completes the JSON line
+    with the headline and whatever secondaries finished, marks the rest as timed out, prints it on
+    rank 0 and ends the process on every rank (os._exit: a rank stuck in a GPU call or collective
+    cannot be joined).  The headline measurement is already done when it starts."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            done = dict(line.get("secondary") or {})
+            for k in keys:
+                done.setdefault(k, {"error": f"timed out after {timeout_s:.0f} s (watchdog)"})
+            out = dict(line, secondary=done)
+            sys.stdout.write(json.dumps(out) + "\n")
+            sys.stdout.flush()
+        sys.stderr.write(f"bench.py: secondary measurements exceeded {timeout_s:.0f} s; exiting\n")
+        sys.stderr.flush()
+        os._exit(0)
+
+    t = threading.Timer(timeout_s, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -536,6 +561,8 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=64, help="cpu_baseline sample size (whole 4096^2 planes)")
     ap.add_argument("--cpu-budget", type=float, default=30.0, help="cpu_baseline time budget, seconds")
     ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 / cfg5 secondary measurements")
+    ap.add_argument("--secondary-timeout", type=float, default=420.0,
+                    help="seconds the cfg3 / cfg4 / cfg5 secondaries may take before the line is printed without them")
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the cpu_baseline leg (e.g. --cpu-planes 64 --cpu-budget 1e9 for the whole sweep)")
     ap.add_argument("--dry-run", action="store_true",
@@ -672,13 +699,18 @@ def main():
         "output_check": {"ok": checks_ok, "planes": checks},
     }
     if not args.headline_only:
-        # secondary workloads never take the headline line down with them
+        # secondary workloads never take the headline line down with them: an exception is reported
+        # in the line, and a secondary still running after --secondary-timeout seconds (a hang, e.g.
+        # in a collective) is reported as such by a watchdog that prints the line and ends every rank
         line["secondary"] = {}
-        for key, fn in (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat), ("cfg5_donn", bench_donn)):
+        secs = (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat), ("cfg5_donn", bench_donn))
+        watchdog = _secondary_watchdog(line, [k for k, _ in secs], rank, args.secondary_timeout)
+        for key, fn in secs:
             try:
                 line["secondary"][key] = fn(dev, rank, world, dist=ranks.dist)
             except Exception as e:  # noqa: BLE001 -- reported in the JSON line
                 line["secondary"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+        watchdog.cancel()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.cpu_planes)
     if rank == 0:

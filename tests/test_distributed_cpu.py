@@ -174,3 +174,22 @@ def test_bench_refuses_gpus_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4", "--dry-run"],
                        capture_output=True, text=True, timeout=300, cwd=root, env=env)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_secondary_watchdog_prints_the_line_and_exits():
+    """A secondary that hangs (e.g. in a collective) must not cost the headline line: the watchdog
+    prints the line with the finished secondaries and the rest marked as timed out, and exits 0."""
+    import json
+    import subprocess
+    import sys
+    code = ("import json, time, bench\n"
+            "line = {'metric': 'm', 'value': 1.0, 'secondary': {}}\n"
+            "bench._secondary_watchdog(line, ['cfg3_czt', 'cfg4_qat'], 0, 0.5)\n"
+            "line['secondary']['cfg3_czt'] = {'value': 2.0}\n"
+            "time.sleep(60)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["value"] == 1.0 and out["secondary"]["cfg3_czt"] == {"value": 2.0}
+    assert "timed out" in out["secondary"]["cfg4_qat"]["error"]
