@@ -257,7 +257,7 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
 // ---------------------------------------------------------------------------------------------
 constexpr int CZB_BS = wf::N / 2;
 
-constexpr int CZB_W = 4;   // rows pass: lines (waves) per workgroup
+constexpr int CZB_W = 8;   // rows pass: lines (waves) per workgroup (8: the twiddle tables are gathered once per 8 lines; 4 -> 8 measured 0.59 -> 0.565 ms at cfg3, profiles/r03_czt_probe.txt)
 constexpr int CZB_WC = CB;  // columns pass: one 16-column block of V per workgroup
 #ifndef CZB_WPE
 #define CZB_WPE 4
