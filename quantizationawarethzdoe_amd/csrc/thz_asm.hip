@@ -817,7 +817,13 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     };
     Mx300::run<true, MX_T>(lds, twr, tid, ld, sv);
   } else if constexpr (PN > 0) {
-    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
+    // The twiddle tables' global loads go out first and their LDS writes happen after the first
+    // stage's gather (the hook runs before the first exchange), so the gather does not wait behind
+    // them: cfg2 K3 4.40 -> 4.28 ms (profiles/r03_k3_probes.txt)
+    constexpr int TT = Geo<PN>::T;
+    const auto twf = tw_fetch<PN, TT>(pw.tw, tid);
+    const TwLds twl = tw_lds_at<PN>(tw_slot<PN>(lds));
+    auto tw_hook = [&]() { tw_store<PN, TT>(tw_slot<PN>(lds), twf, tid); };
     // First stage (radix 16, L = 1) reads j = i + q*NB0, i < NB0.  Its band column is
     // c = c0 + delta_q with c0 = i + J >= 0 and delta_q = q*NB0 (- PN for the negative
     // frequencies), a multiple of CBU: the blocked address is then base(c0) + delta_q*Hout,
@@ -842,7 +848,7 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
       const int w = j - a.out_c0;
       if ((unsigned)w < (unsigned)a.Wout) put(w, v);
     };
-    fft_pow2_run<true, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<true, PN, TT, FFT_ROWS>(lds, twl, tid, ld, sv, tw_hook);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int c = band_col(j, a.Pw, a.J, a.ncols);

@@ -310,7 +310,7 @@ template <bool PARTIAL>
 __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_rows_blk(const float2* __restrict__ in, float2* __restrict__ V,
                                                            const float2* __restrict__ ws, CztArgs a) {
   extern __shared__ float2 lds[];
-  const wf::Tabs tw = wf::fill_tables(lds, a.tw1024, threadIdx.x, blockDim.x);
+  const wf::Tabs tw = wf::fill_tables<64 * CZB_W>(lds, a.tw1024, threadIdx.x);
   float* img = wf::wave_image(lds, threadIdx.x >> 6);
   __syncthreads();
   const int lane = threadIdx.x & 63;

@@ -362,6 +362,40 @@ __device__ __forceinline__ TwLds load_tw_lds(float2* dst, const float2* __restri
   return TwLds{dst, dst + N2};
 }
 
+// The same fill in two halves, so the table's global loads can be issued ahead of a kernel's data
+// loads and written to LDS after them (tw_fetch -> data loads -> tw_store, before the first barrier
+// that precedes a twiddle read): NT threads, each fetching ceil(count / NT) entries into registers.
+template <int N, int NT>
+struct TwFetch {
+  static constexpr int K = (tw_lds_count(N) + NT - 1) / NT;
+  float2 v[K];
+};
+template <int N, int NT>
+__device__ __forceinline__ TwFetch<N, NT> tw_fetch(const float2* __restrict__ tw, int tid) {
+  constexpr int N2 = 64 + N / 64;
+  TwFetch<N, NT> f;
+#pragma unroll
+  for (int k = 0; k < TwFetch<N, NT>::K; ++k) {
+    const int i = tid + k * NT;
+    const int q = i - N2;
+    const int t = i < 64 ? i : (i < N2 ? (i - 64) * 64 : (q >> 4) * (q & 15) * (N / 256));
+    f.v[k] = i < tw_lds_count(N) ? tw[t] : make_float2(0.f, 0.f);
+  }
+  return f;
+}
+template <int N, int NT>
+__device__ __forceinline__ void tw_store(float2* dst, const TwFetch<N, NT>& f, int tid) {
+#pragma unroll
+  for (int k = 0; k < TwFetch<N, NT>::K; ++k) {
+    const int i = tid + k * NT;
+    if (i < tw_lds_count(N)) dst[i] = f.v[k];
+  }
+}
+template <int N>
+__device__ __forceinline__ TwLds tw_lds_at(float2* dst) {
+  return TwLds{dst, dst + 64 + N / 64};
+}
+
 template <int R, class Tw>
 __device__ __forceinline__ void twiddle_powers(const Tw& tw, int kt, float2* w) {
   // w[r] for r = 1..R-1 (forward sign; the inverse applies them conjugated, cmul_tw);
@@ -726,8 +760,12 @@ __host__ __device__ constexpr int split_c(int L) { return L == 1 ? 1 : (L <= 16 
 template <int L>
 __host__ __device__ constexpr int split_lay(int j) { return j + split_c(L) * (j >> split_sh(L)); }
 
-template <bool INV, int N, int T, int MODE, int S = 0, int L = 1, class Tw, class In, class Sv>
-__device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int tid, In& in, Sv& sv) {
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <bool INV, int N, int T, int MODE, int S = 0, int L = 1, class Tw, class In, class Sv, class Hook = NoHook>
+__device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int tid, In& in, Sv& sv,
+                                                  Hook hook = Hook{}) {
   using P = Pow2Sched<N>;
   constexpr int R = P::radix(S, MODE);
   if constexpr (R == 32 && S == 0) {
@@ -764,6 +802,7 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
   constexpr int MB = N / R / T;
   float2 v[MB][R];
   stage_core<R, INV, N, L, T>(tw, tid, in, v);
+  if constexpr (S == 0) hook();  // e.g. the twiddle tables' LDS writes, after the first stage's loads
   if constexpr (S == P::nst(MODE) - 1) {
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
@@ -835,9 +874,9 @@ template <int N>
 __device__ __forceinline__ float2* tw_slot(float2* lds) {
   return lds + lds_split_f2(N);
 }
-template <bool INV, int N, int T, int MODE, class Tw, class Ld, class Sv>
-__device__ __forceinline__ void fft_pow2_run(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
-  fft_pow2_split_io<INV, N, T, MODE>(reinterpret_cast<float*>(lds), tw, tid, ld, sv);
+template <bool INV, int N, int T, int MODE, class Tw, class Ld, class Sv, class Hook = NoHook>
+__device__ __forceinline__ void fft_pow2_run(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv, Hook hook = Hook{}) {
+  fft_pow2_split_io<INV, N, T, MODE>(reinterpret_cast<float*>(lds), tw, tid, ld, sv, hook);
 }
 
 // Whole transform with the data in LDS (natural order in and out).

@@ -70,6 +70,24 @@ __device__ __forceinline__ Tabs fill_tables(float2* tab, const float2* __restric
   for (int t = tid; t < TAB; t += nt) tab[t] = tw1024[tab_source(t)];
   return Tabs{tab + T1024, tab + T512, tab + T256, tab + T64, tab + TINV};
 }
+// The same fill by a workgroup of NT threads with every load issued before the first LDS write (the
+// loop form waits out one L2 round trip per entry it writes)
+template <int NT>
+__device__ __forceinline__ Tabs fill_tables(float2* tab, const float2* __restrict__ tw1024, int tid) {
+  constexpr int K = (TAB + NT - 1) / NT;
+  float2 v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int t = tid + k * NT;
+    v[k] = t < TAB ? tw1024[tab_source(t)] : make_float2(0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int t = tid + k * NT;
+    if (t < TAB) tab[t] = v[k];
+  }
+  return Tabs{tab + T1024, tab + T512, tab + T256, tab + T64, tab + TINV};
+}
 
 // This wave's float image behind the workgroup's tables.  Its offset is made opaque so the
 // compiler keeps the (large, constant) image base in the address register: every exchange access
