@@ -263,7 +263,11 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
     return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
   };
   if constexpr (PN > 0 && !is_mx(PN)) {
-    const TwLds twl = load_tw_lds<PN>(tw_slot<PN>(lds), pw.tw, tid, nt);
+    // twiddle-table loads first, their LDS writes after the row loads (as in K3)
+    constexpr int TT = Geo<PN>::T;
+    const auto twf = tw_fetch<PN, TT>(pw.tw, tid);
+    const TwLds twl = tw_lds_at<PN>(tw_slot<PN>(lds));
+    auto tw_hook = [&]() { tw_store<PN, TT>(tw_slot<PN>(lds), twf, tid); };
     auto ld = [&](int, int, int idx) {
       const int s = idx - a.in_c0;
       return (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
       const int c = band_col(j, PN, a.J, a.ncols);
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
-    fft_pow2_run<false, PN, Geo<PN>::T, FFT_ROWS>(lds, twl, tid, ld, sv);
+    fft_pow2_run<false, PN, TT, FFT_ROWS>(lds, twl, tid, ld, sv, tw_hook);
   } else if constexpr (is_mx(PN)) {
     const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
     auto ld = [&](int, int, int idx) {
