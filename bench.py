@@ -693,6 +693,8 @@ def main():
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in stats.items()},
         "roofline": roof,
+        # every pass on the same footing (K2 and K3 trade places as the longer kernel box to box)
+        "roofline_by_kernel": {k: round(v["gbs_pruned"] / HBM_PEAK_GBS, 4) for k, v in stats.items()},
         "roofline_step": roof_step,
         "roofline_survey_model": roof_model,
         "write_amplification": write_amp,
