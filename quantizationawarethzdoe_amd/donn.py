@@ -24,6 +24,7 @@ import torch
 import torch.nn as nn
 
 from quantizationawarethzdoe_amd import optics as _optics
+from quantizationawarethzdoe_amd.qat import _CAPTURE_MODE
 from quantizationawarethzdoe_amd import propagation as _prop
 from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
 from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
@@ -233,7 +234,7 @@ class DONNTrainer:
                 # no collective, or a captured one: the whole step is one graph, one replay per step
                 try:
                     g_fb = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g_fb):
+                    with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
                         loss = self._fb(su, st, frac)
                         self.allreduce.reduce()
                         self._opt()
@@ -246,9 +247,9 @@ class DONNTrainer:
                     self.capture_collective = False
                     self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_fb):
+            with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
                 loss = self._fb(su, st, frac)
-            with torch.cuda.graph(g_opt):
+            with torch.cuda.graph(g_opt, capture_error_mode=_CAPTURE_MODE):
                 self._opt()
         return g_fb, g_opt, loss
 

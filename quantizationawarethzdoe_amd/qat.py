@@ -34,6 +34,13 @@ from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
 from quantizationawarethzdoe_amd.utils.Helper_Functions import normalize
 from quantizationawarethzdoe_amd.utils.units import m, mm, um
 
+# Graph captures restrict unsafe HIP calls to the capturing thread only.  Under the default
+# ("global") mode, ProcessGroupNCCL's watchdog thread polling its work events while a step is being
+# captured gets hipErrorStreamCaptureUnsupported and aborts the process (seen once in the -m gpu
+# suite, tests/test_collective_capture_gpu.py, one-rank RCCL group).  Captured collectives do not
+# enqueue watchdog work, so the watchdog only ever polls eager work outside the graph.
+_CAPTURE_MODE = "thread_local"
+
 C0 = 2.998e8
 FOCI_MM = [(-20, -20), (20, 20), (-20, 20), (20, -20), (0, 0), (0, -20), (-20, 0), (0, 20), (20, 0)]
 
@@ -337,7 +344,7 @@ class QATTrainer:
                 # one graph, one replay per step
                 try:
                     g_fb = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g_fb):
+                    with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
                         loss = self._fb(frac)
                         self.allreduce.reduce()
                         self._opt()
@@ -349,9 +356,9 @@ class QATTrainer:
                     self.capture_collective = False
                     self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_fb):
+            with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
                 loss = self._fb(frac)
-            with torch.cuda.graph(g_opt):
+            with torch.cuda.graph(g_opt, capture_error_mode=_CAPTURE_MODE):
                 self._opt()
         return g_fb, g_opt, loss
 
