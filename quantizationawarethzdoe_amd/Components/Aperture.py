@@ -69,6 +69,8 @@ class ApertureElement(nn.Module):
     def aperture(self):
         """The mask of the last forward (Components/Aperture.py:112-123 stores it as ``self.aperture``),
         formed on first read instead of on every call."""
+        if "_aperture_set" in self.__dict__:  # assigned by the caller, as the reference's attribute can be
+            return self.__dict__["_aperture_set"]
         src = self.__dict__.get("_aperture_src")
         if src is None:
             raise AttributeError("'ApertureElement' has no aperture before its first forward")
@@ -79,9 +81,14 @@ class ApertureElement(nn.Module):
             return self.add_rect_aperture_to_field(field, rect_height=self.aperture_size, rect_width=self.aperture_size)
         return torch.ones(field.shape, dtype=field.dtype, device=field.device)
 
+    @aperture.setter
+    def aperture(self, mask):
+        self.__dict__["_aperture_set"] = mask
+
     def forward(self, field: ElectricField) -> ElectricField:
         dx, dy = field.spacing_host
         H, W = field.height, field.width
+        self.__dict__.pop("_aperture_set", None)
         self.__dict__["_aperture_src"] = (self.aperture_type, types.SimpleNamespace(
             spacing_host=field.spacing_host, height=H, width=W, shape=tuple(field.shape), dtype=field.data.dtype,
             device=field.device))
