@@ -777,6 +777,7 @@ __device__ __forceinline__ void fft_pow2_split_io(float* lds, const Tw& tw, int 
     constexpr int MB2 = NB2 / T;
     float2 v1[16];
     stage_r32_pair_first<INV, N>(tid, in, v1);
+    hook();
     float2 nx[MB2][16];
     float* dst = lds + split_lay<1>(32 * pair_i(tid) + ((tid >> 5) & 1));
 #pragma unroll
