@@ -42,11 +42,11 @@ class _PendingAsm:
         self.prop, self.field, self.zs = prop, field, zs
 
     def run(self):
-        return self.prop._run(self.field, self.zs)[0]
+        return self.prop._run(self.field, self.zs).squeeze(0)
 
     def run_loss(self, target):
         out, loss = self.prop._run(self.field, self.zs, loss_target=target)
-        return out[0], loss
+        return out.squeeze(0), loss
 
 
 class ASM_prop(nn.Module):
@@ -270,7 +270,10 @@ class ASM_prop(nn.Module):
             Eout._pending = _PendingAsm(self, field, self._zh)
             return Eout
         out = self._run(field, self._zh)
-        Eout = ElectricField(data=out[0], wavelengths=field.wavelengths, spacing=field.spacing, device=field.device)
+        # squeeze, not out[0]: a select's backward materialises a zero [1, B, C, H, W] gradient and
+        # copies into it, a squeeze's is a view (one fill and one copy kernel fewer per backward)
+        Eout = ElectricField(data=out.squeeze(0), wavelengths=field.wavelengths, spacing=field.spacing,
+                             device=field.device)
         return Eout._adopt_host(field)
 
     def propagate_planes(self, field: ElectricField, z_list) -> torch.Tensor:
