@@ -561,7 +561,7 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=64, help="cpu_baseline sample size (whole 4096^2 planes)")
     ap.add_argument("--cpu-budget", type=float, default=30.0, help="cpu_baseline time budget, seconds")
     ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 / cfg5 secondary measurements")
-    ap.add_argument("--secondary-timeout", type=float, default=420.0,
+    ap.add_argument("--secondary-timeout", type=float, default=300.0,
                     help="seconds the cfg3 / cfg4 / cfg5 secondaries may take before the line is printed without them")
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the cpu_baseline leg (e.g. --cpu-planes 64 --cpu-budget 1e9 for the whole sweep)")
