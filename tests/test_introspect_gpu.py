@@ -96,6 +96,51 @@ def test_asm_create_kernel_matches_reference(G, name, capsys):
     assert capsys.readouterr().out == ""
 
 
+def _np_angle(H, W, s, dx, dy, lam, z, do_padding=True):
+    """The reference's fp32 angle z sqrt(k^2 - K^2) on the centred padded grid, op by op in numpy fp32
+    (Props/ASM_Prop.py:141-145, 244-253)."""
+    f32 = np.float32
+    ph, pw = (int(np.floor(s * H / 2)), int(np.floor(s * W / 2))) if do_padding else (0, 0)
+    Ph, Pw = H + 2 * ph, W + 2 * pw
+    kx = (f32(2 * np.pi) * ((np.arange(Ph, dtype=f32) - f32(Ph // 2)) / f32(Ph))) / f32(dx)
+    ky = (f32(2 * np.pi) * ((np.arange(Pw, dtype=f32) - f32(Pw // 2)) / f32(Pw))) / f32(dy)
+    k = f32(2 * np.pi) / np.asarray(lam, dtype=f32)[:, None, None]
+    with np.errstate(invalid="ignore"):
+        return f32(z) * np.sqrt(k * k - (kx[:, None] * kx[:, None] + ky[None, :] * ky[None, :]))
+
+
+def test_asm_create_kernel_random_geometries_vs_oracle_masks():
+    """create_kernel on seeded random geometries (sizes 8-160, padding 0-2.5, 1-3 wavelengths,
+    |z| up to 0.4 m, every band-limit setting): the masks equal the oracle's
+    (oracle.asm_transfer_function, pinned to the reference's create_kernel by the CPU tests) exactly,
+    and the values equal exp(i angle) of the reference's fp32 angle to 1e-6."""
+    from oracle import thz_oracle as orc
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(11)
+    for _ in range(24):
+        H, W = int(rng.integers(8, 161)), int(rng.integers(8, 161))
+        s = float(rng.choice([0.0, 0.5, 1.0, 1.5, 2.0, 2.5]))
+        nl = int(rng.integers(1, 4))
+        freqs = [float(f) for f in rng.uniform(150, 450, nl)]
+        dx, dy = float(rng.uniform(0.2, 1.5)) * MM, float(rng.uniform(0.2, 1.5)) * MM
+        z = float(rng.uniform(-0.4, 0.4))
+        bl, bt = [(True, "exact"), (True, "approx"), (False, "exact")][int(rng.integers(0, 3))]
+        wl = [C0 / (f * 1e9) for f in freqs]
+        f = ElectricField(torch.ones((1, nl, H, W), dtype=torch.complex64, device=dev),
+                          wavelengths=wl if nl > 1 else wl[0], spacing=[dx, dy], device=dev)
+        prop = ASM_prop(z_distance=z, padding_scale=s, bandlimit_kernel=bl, bandlimit_type=bt, device=dev)
+        prop.check_Zc = False
+        got = prop.create_kernel(f).cpu().numpy()
+        lam = torch.tensor(wl, dtype=torch.float32)
+        Ph, Pw = got.shape[-2:]
+        ref = orc.asm_transfer_function(Ph, Pw, lam, torch.tensor(dx, dtype=torch.float32),
+                                        torch.tensor(dy, dtype=torch.float32), z, bl, bt).numpy()
+        np.testing.assert_array_equal(got == 0, ref == 0, err_msg=f"{H}x{W} s={s} z={z} {bl} {bt}")
+        ang = _np_angle(H, W, s, dx, dy, np.array(wl, dtype=np.float32), z)
+        exact = np.where(ref != 0, np.exp(1j * np.nan_to_num(ang).astype(np.float64)), 0)[None]
+        assert np.abs(got - exact).max() <= 1e-6, (H, W, s, z, bl, bt)
+
+
 def test_asm_kernel_is_what_forward_applies():
     """The exported table is the transfer function the propagation kernels apply on the fly:
     crop(ifft2(fft2(pad x) * ifftshift(H))) with torch's FFT on the exported H equals forward(x)."""
