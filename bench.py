@@ -77,9 +77,11 @@ def shard_planes(n_planes, rank, world):
     return list(range(start, start + base + (1 if rank < extra else 0)))
 
 
-def z_planes(rank, world):
-    """This rank's share of the global sweep (weak scaling: Z_PER_RANK planes per rank)."""
-    total = Z_PER_RANK * world
+def z_planes(rank, world, split="weak"):
+    """This rank's share of the global sweep: weak scaling (the default) gives every rank Z_PER_RANK
+    planes of a Z_PER_RANK * world sweep; strong scaling splits the 64-plane cfg2 sweep itself over
+    the ranks (8 z per GPU at N = 8)."""
+    total = Z_PER_RANK * world if split == "weak" else Z_PER_RANK
     zs = torch.linspace(Z_MIN, Z_MAX, total, dtype=torch.float64)
     return [float(zs[i]) for i in shard_planes(total, rank, world)]
 
@@ -385,17 +387,64 @@ def bench_donn(dev, rank, world, steps=20, warmup=3, dist=None):
                         "replay; synthetic digits", "per_rank_batch": per, "modes": out}
 
 
+def per_rank_shares(dev, x, lam, sp, world=8):
+    """One GPU timing the work ONE rank of an 8-GPU run gets when each workload is split over the
+    ranks (strong scaling): cfg2's 64-plane sweep at 8 planes, cfg3's 32 wavelengths at 4, cfg5's
+    batch of 256 at 32.  Per-rank times, not a scaling claim: the 8-GPU step takes at least the
+    slowest rank's share, so share_time x 8 / full_time is the efficiency a strong split can reach
+    (the cfg3 columns pass, e.g., has 8x fewer lines to fill the chip with)."""
+    from quantizationawarethzdoe_amd.propagation import asm_apply
+    from quantizationawarethzdoe_amd import _lib
+    zs = z_planes(0, world, "strong")
+    out = torch.empty((len(zs), 1, 1, N_FIELD, N_FIELD), dtype=torch.complex64, device=dev)
+    pad = N_FIELD // 2
+
+    def step():
+        asm_apply(x, lam, sp, zs, pad, pad, True, 1, out=out)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    _lib.timing_reset()
+    _lib.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / 10
+    _lib.timing_enable(False)
+    kern = {}
+    for k in ("asm_rows_fwd", "asm_cols", "asm_rows_inv"):
+        ms, n = _lib.timing_read(k)
+        if n:
+            kern[k] = round(ms / n, 4)
+    chk = check_plane(out[0, 0, 0], zs[0])
+    cfg2 = {"planes": len(zs), "ms_per_step": round(dt * 1e3, 3), "planes_per_s": round(len(zs) / dt, 1),
+            "kernel_avg_ms": kern, "output_check": chk}
+    czt = bench_czt(dev, 0, world)
+    donn = bench_donn(dev, 0, world)
+    return {"note": "one GPU timing one rank's share of an 8-GPU strong split; per-rank times, not a scaling "
+                    "measurement", "cfg2_8_planes": cfg2,
+            "cfg3_4_wavelengths": {k: czt[k] for k in ("ms_per_call", "kernel_avg_ms", "output_check")},
+            "cfg5_batch_32": {m: {k: v[k] for k in ("ms_per_step", "output_check")} for m, v in donn["modes"].items()}}
+
+
 def load_traffic():
-    """HBM bytes per launch of each kernel from the committed rocprofv3 PMC summary
-    (scripts/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) x 1 KiB, the gfx950 correction)."""
+    """(HBM bytes per launch of each kernel, where they come from): the committed rocprofv3 PMC
+    summary (scripts/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) x 1 KiB, the gfx950 correction),
+    written by a separate profiling run -- NOT measured in this bench run (PMC counters need their
+    own rocprofv3 passes); ``_meta`` names the profile and the kernel build it was taken on."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
-        return None
+        return None, None
     try:
         with open(path) as fh:
-            return json.load(fh)
+            d = json.load(fh)
     except Exception:
-        return None
+        return None, None
+    meta = d.pop("_meta", None) or {}
+    src = (f"profiles/pmc_traffic.json from rocprofv3 PMC passes ({meta.get('profile', 'profile unnamed')}, "
+           f"{meta.get('date', 'date unrecorded')}); a separate profiling run, not this bench run")
+    return d, src
 
 
 def cpu_model():
@@ -526,24 +575,55 @@ def launch_ranks(args):
     sys.exit(subprocess.call(cmd))
 
 
-def _secondary_watchdog(line, keys, rank, timeout_s):
+def _failed_checks(secondary):
+    """The secondaries whose output check ran and failed (a wrong result), as strings: every
+    ``output_check`` at any depth of a secondary's result (its modes, the per-rank shares)."""
+    failed = []
+
+    def walk(key, d):
+        if not isinstance(d, dict) or "error" in d:
+            return
+        chk = d.get("output_check")
+        if isinstance(chk, dict) and not chk.get("ok"):
+            failed.append(f"{key}: {chk}")
+        for k, v in d.items():
+            if k != "output_check" and isinstance(v, dict):
+                walk(f"{key}.{k}", v)
+    for key, sec in (secondary or {}).items():
+        walk(key, sec)
+    return failed
+
+
+WATCHDOG_EXIT = 4  # the secondaries outlived --secondary-timeout: the run did not finish
+
+
+def _secondary_watchdog(line, keys, rank, timeout_s, snapshot):
     """A timer that, should the secondary measurements outlive ``timeout_s``, completes the JSON line
     with the headline and whatever secondaries finished, marks the rest as timed out, prints it on
-    rank 0 and ends the process on every rank (os._exit: a rank stuck in a GPU call or collective
-    cannot be joined).  The headline measurement is already done when it starts."""
+    rank 0 and ends the process on every rank with WATCHDOG_EXIT (os._exit: a rank stuck in a GPU
+    call or collective cannot be joined; a hang is a failure, not a success).  The headline
+    measurement is already done when it starts.  ``snapshot`` is a list the main thread replaces
+    with a finished copy of the secondaries after each one, so the timer never reads a dict that
+    is being written; any failure inside the timer still ends in os._exit."""
     import threading
 
     def fire():
-        if rank == 0:
-            done = dict(line.get("secondary") or {})
+        try:
+            done = dict(snapshot[0]) if snapshot else {}
             for k in keys:
                 done.setdefault(k, {"error": f"timed out after {timeout_s:.0f} s (watchdog)"})
-            out = dict(line, secondary=done)
-            sys.stdout.write(json.dumps(out) + "\n")
-            sys.stdout.flush()
-        sys.stderr.write(f"bench.py: secondary measurements exceeded {timeout_s:.0f} s; exiting\n")
-        sys.stderr.flush()
-        os._exit(0)
+            if rank == 0:
+                out = dict(line, secondary=done)
+                sys.stdout.write(json.dumps(out) + "\n")
+                sys.stdout.flush()
+            failed = _failed_checks(done)
+            sys.stderr.write(f"bench.py: secondary measurements exceeded {timeout_s:.0f} s; exiting "
+                             f"with status {WATCHDOG_EXIT}\n")
+            if failed:
+                sys.stderr.write("bench.py: output check FAILED:\n  " + "\n  ".join(failed) + "\n")
+            sys.stderr.flush()
+        finally:
+            os._exit(WATCHDOG_EXIT)
 
     t = threading.Timer(timeout_s, fire)
     t.daemon = True
@@ -565,6 +645,10 @@ def main():
                     help="seconds the cfg3 / cfg4 / cfg5 secondaries may take before the line is printed without them")
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the cpu_baseline leg (e.g. --cpu-planes 64 --cpu-budget 1e9 for the whole sweep)")
+    ap.add_argument("--cfg2-split", choices=("weak", "strong"), default="weak",
+                    help="weak: 64 z-planes per rank (the default line); strong: the 64-plane sweep split over the ranks")
+    ap.add_argument("--no-shares", action="store_true",
+                    help="skip the one-GPU timing of the per-rank shares of an 8-GPU run (world size 1 only)")
     ap.add_argument("--dry-run", action="store_true",
                     help="rehearse the rank orchestration on the CPU (gloo, propagation stubbed, no GPU)")
     args = ap.parse_args()
@@ -574,7 +658,8 @@ def main():
     launch_ranks(args)
     ranks = Ranks(args.dry_run)
     rank, world, dev = ranks.rank, ranks.world, ranks.dev
-    zs = z_planes(rank, world)
+    zs = z_planes(rank, world, args.cfg2_split)
+    total_planes = Z_PER_RANK * world if args.cfg2_split == "weak" else Z_PER_RANK
     if args.dry_run:
         done = []
         seen = torch.zeros(1, dtype=torch.float64)
@@ -583,13 +668,14 @@ def main():
             done.append(len(zs))
             seen.add_(sum(zs))
         elapsed = timed(step, args.steps, args.warmup, ranks)
-        planes = Z_PER_RANK * world * args.steps
-        cover = sorted(i for r in ranks.gather(shard_planes(Z_PER_RANK * world, rank, world)) for i in r)
+        planes = total_planes * args.steps
+        cover = sorted(i for r in ranks.gather(shard_planes(total_planes, rank, world)) for i in r)
         lam_cover = sorted(i for r in ranks.gather(shard_planes(32, rank, world)) for i in r)  # cfg3 λ shards
         batch_cover = sorted(i for r in ranks.gather(shard_planes(256, rank, world)) for i in r)  # cfg5 batch
         if rank == 0:
             print(json.dumps({"metric": METRIC, "value": round(planes / elapsed, 2), "unit": "propagations/s",
                               "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "dry_run": True,
+                              "scaling": args.cfg2_split,
                               "planes_per_rank_step": done[-1], "planes_covered": cover,
                               "wavelengths_covered": lam_cover, "samples_covered": batch_cover,
                               "elapsed_max_s": elapsed}), flush=True)
@@ -619,7 +705,7 @@ def main():
     checks = [c for c in (check_plane(out[0, 0, 0], zs[0]), check_plane(out[-1, 0, 0], zs[-1])) if c]
     checks_ok = all(ranks.gather(all(c["ok"] for c in checks)))
 
-    planes = Z_PER_RANK * world * args.steps
+    planes = total_planes * args.steps
     value = planes / elapsed
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -636,7 +722,8 @@ def main():
              "asm_rows_inv": 8 * zc * (H * Pw + H * W)}
     pruned = {"asm_rows_fwd": 8 * (H * W + ncols * H), "asm_cols": 8 * (ncols * H + zc * ncols * H),
               "asm_rows_inv": 8 * (zc * ncols * H + zc * H * W)}
-    traffic = load_traffic() or {}
+    traffic, traffic_src = load_traffic()
+    traffic = traffic or {}
     stats = {}
     for k, (ms, n) in kern.items():
         if n:
@@ -650,7 +737,7 @@ def main():
     total_alg = sum(pruned[k] * stats[k]["launches"] for k in stats) / args.steps
     total_pmc = (sum(traffic[k] * stats[k]["launches"] for k in stats) / args.steps
                  if all(traffic.get(k) for k in stats) else None)
-    roof = roof_model = roof_step = None
+    roof = roof_model = roof_step = roof_ns = None
     if dom:
         # roofline.achieved = the bytes the dominant kernel must move (the band-pruned minimum: only
         # the ncols spectral columns that can be non-zero, the column spectrum kept in registers)
@@ -660,12 +747,21 @@ def main():
                 "unit": "GB/s", "frac": round(stats[dom]["gbs_pruned"] / HBM_PEAK_GBS, 4),
                 "traffic": traffic.get(dom),
                 "traffic_gbs": round(stats[dom]["gbs_pmc"], 1) if "gbs_pmc" in stats[dom] else None,
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": pruned[dom], "avg_launch_ms": round(stats[dom]["avg_ms"], 4),
                 "bytes_model": f"band-pruned minimum per launch ({ncols} of {Pw} spectral columns can be non-zero; "
                                f"K2 keeps each column spectrum in registers across the z-chunk): K1 8(HW + ncols H), "
                                f"K2 8(ncols H + zc ncols H), K3 8 zc (ncols H + HW); traffic = PMC (2 FETCH_SIZE + "
                                f"WRITE_SIZE) bytes per launch (profiles/pmc_traffic.json)"}
         # the whole step on the same bytes: every kernel's minimum / the measured step time
+        # north_star's graded kernel, whichever pass dominates: the FFT + transfer-function column
+        # pass (K2) on its band-pruned minimum bytes
+        if "asm_cols" in stats:
+            k2 = stats["asm_cols"]
+            roof_ns = {"kernel": "asm_cols (K2: column FFT + transfer function, north_star's kernel)",
+                       "achieved": round(k2["gbs_pruned"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                       "frac": round(k2["gbs_pruned"] / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": pruned["asm_cols"],
+                       "avg_launch_ms": round(k2["avg_ms"], 4), "target_frac": 0.40}
         roof_step = {"achieved": round(total_alg / (ms_per_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(total_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": total_alg}
@@ -676,16 +772,18 @@ def main():
                       "alg_bytes_per_launch": model[dom],
                       "bytes_model": "SURVEY §8(d) 3-pass model, z_chunk planes per launch"}
     write_amp = {k: round(traffic[k] / pruned[k], 3) for k in stats if traffic.get(k)}
-    step_model = 8 * (H * W + H * Pw + Z_PER_RANK * (3 * H * Pw + H * W))
+    step_model = 8 * (H * W + H * Pw + len(zs) * (3 * H * Pw + H * W))
 
     line = {
         "metric": METRIC, "value": round(value, 2), "unit": "propagations/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "complex64 (fp32)",
+        "higher_is_better": True, "scaling": args.cfg2_split, "vs_baseline": None, "dtype": "complex64 (fp32)",
         "data": "synthetic (Gaussian beam generated on device)",
-        "config": {"workload": "cfg2: ASM_prop 4096x4096 Gaussian_beam -> 64 z-planes/GPU (20-120 mm), "
-                               "300 GHz, dx 0.25 mm, padding_scale 1 (P=8192), exact band limit",
-                   "planes_per_step_per_gpu": Z_PER_RANK, "N": N_FIELD, "P": 2 * N_FIELD,
+        "config": {"workload": ("cfg2: ASM_prop 4096x4096 Gaussian_beam -> 64 z-planes/GPU (20-120 mm), "
+                                if args.cfg2_split == "weak" else
+                                "cfg2: ASM_prop 4096x4096 Gaussian_beam -> 64 z-planes (20-120 mm) split over the GPUs, ")
+                               + "300 GHz, dx 0.25 mm, padding_scale 1 (P=8192), exact band limit",
+                   "planes_per_step_per_gpu": len(zs), "N": N_FIELD, "P": 2 * N_FIELD,
                    "band_columns": ncols, "z_chunk": zc, "parallelism": f"z-shard x{world}"},
         "hbm_gbs_band_pruned": round(total_alg * args.steps / elapsed / 1e9 * world, 1),
         "hbm_gbs_survey_model": round(step_model * args.steps / elapsed / 1e9 * world, 1),
@@ -695,6 +793,7 @@ def main():
         "roofline": roof,
         # every pass on the same footing (K2 and K3 trade places as the longer kernel box to box)
         "roofline_by_kernel": {k: round(v["gbs_pruned"] / HBM_PEAK_GBS, 4) for k, v in stats.items()},
+        "roofline_north_star": roof_ns,
         "roofline_step": roof_step,
         "roofline_survey_model": roof_model,
         "write_amplification": write_amp,
@@ -704,15 +803,26 @@ def main():
         # secondary workloads never take the headline line down with them: an exception is reported
         # in the line, and a secondary still running after --secondary-timeout seconds (a hang, e.g.
         # in a collective) is reported as such by a watchdog that prints the line and ends every rank
-        line["secondary"] = {}
+        secondary = {}
+        snapshot = [{}]
         secs = (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat), ("cfg5_donn", bench_donn))
-        watchdog = _secondary_watchdog(line, [k for k, _ in secs], rank, args.secondary_timeout)
+        watchdog = _secondary_watchdog(line, [k for k, _ in secs], rank, args.secondary_timeout, snapshot)
         for key, fn in secs:
             try:
-                line["secondary"][key] = fn(dev, rank, world, dist=ranks.dist)
+                res = fn(dev, rank, world, dist=ranks.dist)
             except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-                line["secondary"][key] = {"error": f"{type(e).__name__}: {e}"[:300]}
+                res = {"error": f"{type(e).__name__}: {e}"[:300]}
+            secondary[key] = res
+            snapshot[0] = dict(secondary)  # one reference swap: the watchdog reads a finished copy
+        if world == 1 and not args.no_shares:
+            try:
+                res = per_rank_shares(dev, x, lam, sp)
+            except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+                res = {"error": f"{type(e).__name__}: {e}"[:300]}
+            secondary["per_rank_share_n8"] = res
+            snapshot[0] = dict(secondary)
         watchdog.cancel()
+        line["secondary"] = secondary
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.cpu_planes)
     if rank == 0:
@@ -720,16 +830,9 @@ def main():
     ranks.close()
     failed = [] if checks_ok else [f"cfg2 headline: {checks}"]
     for key, sec in (line.get("secondary") or {}).items():
-        if sec is None:
-            continue
-        if "error" in sec:  # reported in the line; only a wrong result fails the run
+        if isinstance(sec, dict) and "error" in sec:  # reported in the line; only a wrong result fails the run
             sys.stderr.write(f"bench.py: {key} did not run: {sec['error']}\n")
-            continue
-        parts = [sec] if "output_check" in sec else list((sec.get("modes") or {}).values())
-        for part in parts:
-            chk = part.get("output_check")
-            if chk is not None and not chk.get("ok"):
-                failed.append(f"{key}: {chk}")
+    failed += _failed_checks(line.get("secondary"))
     if failed:
         sys.stderr.write("bench.py: output check FAILED:\n  " + "\n  ".join(failed) + "\n")
         sys.exit(3)

@@ -223,6 +223,10 @@ class ASM_prop(nn.Module):
         self._zc_diagnostic(H + 2 * ph, sp[0], wl, zs[0])
         x = _prop.kernel_dtype(data, "ASM_prop", field.wavelengths)
         unpad = (not self.do_padding) or self.do_unpad_after_pad
+        if loss_target is not None and x.dtype != torch.complex64:
+            # the fused ASM -> loss pipeline and the loss kernel compute in complex64 (the unfused
+            # field_intensity_mse refuses a complex128 field the same way, optics.intensity_mse)
+            raise TypeError(f"loss kernel computes in complex64 fields; got {x.dtype}")
         try:
             if loss_target is not None:
                 fuse = pend is not None and pend.out is None

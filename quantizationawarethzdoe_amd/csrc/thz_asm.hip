@@ -29,6 +29,7 @@
 
 #include "thz_common.hpp"
 #include "thz_dev.hpp"
+#include "thz_wfft.hpp"
 
 
 namespace thz {
@@ -587,6 +588,216 @@ __global__ void __launch_bounds__(1024) asm_cols_zsum(const float2* __restrict__
   asm_cols_body<PN, true>(T, U, ph, a);
 }
 
+// ---------------------------------------------------------------------------------------------
+// K2 at Ph = 8192 as a four-step transform (the cfg2 column pass).  The per-z inverse
+//   y[1024 n1 + n2] = sum_k1 w8^(n1 k1) w8192^(n2 k1) Z_k1[n2],  Z_k1 = IDFT_1024(X[k1 + 8 k2])
+// runs the eight 1024-point transforms Z_k1 one per wave, with no workgroup barrier inside them,
+// and the radix-8 step across the waves after ONE workgroup exchange; the asm_cols kernel runs
+// three radix-16/32 stages behind two workgroup exchanges (four barriers per z).  Per z:
+//   1. x[j] = X[k1 + 8 (lane + 64 j)] H_z (spectrum and sqrt(k^2 - K^2) in registers, as asm_cols)
+//   2. radix 16 over j (k2 = lane + 64 j: in-lane), twiddle w1024^(lane c)
+//   3. 64-point transform over the lane index a = e + 16 f: v_permlane32/16_swap trade lane bits
+//      5, 4 (f) for register bits 0, 1; radix 4 over f in registers, twiddle w64^(g e); one
+//      wave-private LDS exchange (this wave's slice); radix 16 over e.  Lane l then holds
+//      Z_k1[l + 64 h], h < 16.
+//   4. Z_k1 to the slice, barrier, and each thread runs the radix 8 over k1 for n2 = lane +
+//      64 (2 wave + s), s < 2, storing rows 1024 n1 + n2 of the crop: consecutive lanes write
+//      consecutive rows (the U layout and K3 are unchanged).
+// Two barriers per z: before the slice exchange (the previous z's radix-8 reads are done) and
+// after the Z_k1 writes.  The index maps are checked by a numpy model of this data flow and by
+// the cfg2 parity tests.  Props/ASM_Prop.py:314-378 (the per-z ift2 over the padded column).
+namespace fs {
+constexpr int N = 8192, T = 512;
+constexpr int SL = 64 * 17;  // float2 per wave slice: the exchange image (g, c) x e padded to 17
+constexpr int IMG = 8706;    // >= lds_floats2(8192) (the forward transform's image) and 8 SL
+constexpr int TINV = 15 * 64;  // w1024^(lane c), [c - 1][lane]
+constexpr int T64 = 3 * 16;    // w64^(g e), [g - 1][e]
+constexpr int TW8 = 64 + 16;   // w8192^n2 = w8192^(n2 & 63) w128^(n2 >> 6), n2 < 1024
+static_assert(IMG >= 8 * SL && IMG >= lds_floats2(N), "slice region");
+__host__ __device__ constexpr size_t lds_bytes(int nz) {
+  return (size_t)(IMG + TINV + T64 + TW8) * sizeof(float2) + 4 * nz;
+}
+}  // namespace fs
+
+__device__ __forceinline__ void swap_rows16(float& a, float& b) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(b), false, false);
+  a = __int_as_float(r[0]);
+  b = __int_as_float(r[1]);
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  constexpr int PN = fs::N, TT = fs::T;
+  extern __shared__ float2 lds[];
+  float2* const tinv = lds + fs::IMG;
+  float2* const t64 = tinv + fs::TINV;
+  float2* const tw8 = t64 + fs::T64;
+  int* const mz = reinterpret_cast<int*>(tw8 + fs::TW8);
+  int id, z_lo = 0, z_hi = a.nz;
+  if ((int)blockIdx.x < a.kfull) {
+    id = xcd_chunk(blockIdx.x, a.kfull);
+  } else {
+    const int t = blockIdx.x - a.kfull, part = t % a.kparts;
+    id = a.kfull + t / a.kparts;
+    z_lo = part * a.nz / a.kparts;
+    z_hi = (part + 1) * a.nz / a.kparts;
+  }
+  const int bc = id / a.ncols, c = id - bc * a.ncols;
+  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
+  const float lam = a.lam[bc % a.C];
+  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const float2* __restrict__ tw = ph.tw;  // exp(-2 pi i t / 8192)
+  for (int i = tid; i < fs::TINV; i += TT) tinv[i] = tw[8 * (i & 63) * ((i >> 6) + 1)];
+  if (tid < fs::T64) t64[tid] = tw[128 * ((tid >> 4) + 1) * (tid & 15)];
+  if (tid < fs::TW8) tw8[tid] = tw[tid < 64 ? tid : 64 * (tid - 64)];
+  // kept rows |m_x| <= M_z per z (bisection with the reference-order tests, as asm_cols)
+  {
+    for (int zz = tid; zz < z_hi - z_lo; zz += TT) {
+      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + zz]);
+      int lo = -1, hi = PN / 2 + 1;
+      if (tf_pass(a.bl, a.Ph, a.dx, s, Ky, 0)) {
+        lo = 0;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (tf_pass(a.bl, a.Ph, a.dx, s, Ky, mid)) lo = mid;
+          else hi = mid;
+        }
+      }
+      mz[zz] = lo;
+    }
+  }
+  // forward transform of the zero-padded column (once): thread tid holds X[tid + 512 r]
+  float2 sp[16];
+  {
+    int tf = tid;
+    asm volatile("" : "+v"(tf));
+    auto ld0 = [&](int, int, int idx) {
+      const int s = idx - a.in_r0;
+      return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
+    };
+    // 1 / (Ph Pw) is a power of two: scaling the spectrum once is exact
+    auto sv0 = [&](int, int r, int, float2 v) { sp[r] = cscale(v, a.scale); };
+    fft_pow2_io<false, PN, TT, 1, false, false>(lds, tw, tf, ld0, sv0);
+  }
+  // redistribute: wave w takes X[w + 8 (lane + 64 j)] (image k + (k >> 5): both access patterns
+  // conflict-free)
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int k = tid + 512 * r;
+    lds[k + (k >> 5)] = sp[r];
+  }
+  __syncthreads();
+  float sq[16];
+  {
+    const float kl = TWO_PI_F / lam;
+    const float kl2 = tf_mul(kl, kl);
+    const float Ky2 = tf_mul(Ky, Ky);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = w + 8 * (lane + 64 * j);
+      sp[j] = lds[k + (k >> 5)];
+      const float Kx = kfreq(freq_index(k, PN), PN, a.dx);
+      sq[j] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
+    }
+  }
+  for (int zz = z_lo; zz < z_hi; ++zz) {
+    const float z = a.zv[a.zoff + zz];
+    const int M = mz[zz - z_lo];
+    // inputs j in [4, 12) are |m_x| >= PN / 4: zero for every lane when M < PN / 4
+    const bool mid0 = __builtin_amdgcn_readfirstlane(M) < PN / 4;
+    // per-iteration opaque copy of the lane index: otherwise the compiler hoists every
+    // lane-dependent address and predicate of the loop body out of it and spills
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int kb = w + 8 * lane;  // element j is k = kb + 512 j
+    float2 x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      x[j] = make_float2(0.f, 0.f);
+      if (j >= 4 && j < 12 && mid0) continue;
+      // |m_x| = k (j < 8) or PN - k (j >= 8)
+      if (j < 8 ? kb + 512 * j > M : PN - 512 * j - kb > M) continue;
+      float sn, cs;
+      sincos_hw(tf_mul(z, sq[j]), &sn, &cs);
+      x[j] = cmul(sp[j], make_float2(cs, a.adjoint ? -sn : sn));
+    }
+    // step 1: radix 16 over j, then w1024^(+lane c)
+    dft16<true>(x);
+#pragma unroll
+    for (int q = 1; q < 16; ++q) x[q] = cmulc(x[q], tinv[(q - 1) * 64 + lane]);
+    // lane bit 5 <-> register bit 0, lane bit 4 <-> register bit 1: lane e + 16 c1 + 32 c0,
+    // register f1 + 2 f0 + 4 u (u = c >> 2)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      swap_halves(x[2 * p].x, x[2 * p + 1].x);
+      swap_halves(x[2 * p].y, x[2 * p + 1].y);
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (q & 2) continue;
+      swap_rows16(x[q].x, x[q + 2].x);
+      swap_rows16(x[q].y, x[q + 2].y);
+    }
+    // radix 4 over f = f0 + 2 f1 (registers 4u + {0, 2, 1, 3}); output g at 4u + {0, 2, 1, 3}
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float2* v = &x[4 * u];
+      dft4<true>(v[0], v[2], v[1], v[3]);
+      v[2] = cmulc(v[2], t64[lane & 15]);
+      v[1] = cmulc(v[1], t64[16 + (lane & 15)]);
+      v[3] = cmulc(v[3], t64[32 + (lane & 15)]);
+    }
+    __syncthreads();  // A: the previous z's radix-8 reads of every slice are done
+    float2* const slice = lds + w * fs::SL;
+    // exchange image positions: write (g, c, e) at (16 g + c) 17 + e from lane e + 16 c1 + 32 c0,
+    // read e at 17 lane + e
+    const int xw = ((lane >> 5) + 2 * ((lane >> 4) & 1)) * 17 + (lane & 15);
+    const int xr = 17 * lane;
+#pragma unroll
+    for (int rho = 0; rho < 16; ++rho) {
+      const int u = rho >> 2, g = ((rho & 1) << 1) | ((rho >> 1) & 1);
+      slice[xw + (16 * g + 4 * u) * 17] = x[rho];
+    }
+    wf::wave_sync();
+#pragma unroll
+    for (int e = 0; e < 16; ++e) x[e] = slice[xr + e];
+    dft16<true>(x);  // x[h] = Z_k1[lane + 64 h]
+    wf::wave_sync();
+#pragma unroll
+    for (int h = 0; h < 16; ++h) slice[lane + 64 * h] = x[h];
+    __syncthreads();  // B: every Z_k1 is in its slice
+    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int n2 = lane + 64 * (2 * w + s);
+      float2 v[8];
+#pragma unroll
+      for (int k1 = 0; k1 < 8; ++k1) v[k1] = lds[k1 * fs::SL + n2];
+      // the radix-8 step's twiddles w8192^(n2 k1): w8192^n2 from the two-level table, its powers
+      // formed here (no global loads in the z loop: a load behind the previous z's U stores would
+      // wait for them, vmcnt counts in order)
+      const float2 w1 = cmul(tw8[lane], tw8[64 + 2 * w + s]);
+      const float2 w2 = cmul(w1, w1), w3 = cmul(w1, w2), w4 = cmul(w2, w2);
+      v[1] = cmulc(v[1], w1);
+      v[2] = cmulc(v[2], w2);
+      v[3] = cmulc(v[3], w3);
+      v[4] = cmulc(v[4], w4);
+      v[5] = cmulc(v[5], cmul(w1, w4));
+      v[6] = cmulc(v[6], cmul(w2, w4));
+      v[7] = cmulc(v[7], cmul(w3, w4));
+      dft8<true>(v);
+#pragma unroll
+      for (int n1 = 0; n1 < 8; ++n1) {
+        const int r = 1024 * n1 + n2 - a.out_r0;
+        // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2)
+        if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v[n1];
+      }
+    }
+  }
+}
+
 // Per (wavelength, band column) of a mixed-radix Ph: sqrt(k^2 - Kx^2 - Ky^2) of every row
 // (z-independent, written on the first z-chunk) and the kept-row bound M_z of each z of the
 // chunk (bisection with the exact reference-order tests, one lane per z; see asm_cols).  Every
@@ -1106,6 +1317,9 @@ static int ensure_lds_attr() {
     const hipError_t e = hipFuncSetAttribute((const void*)asm_cols_pair<8192>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, mxp);
     if (e != hipSuccess) err = e;
+    const hipError_t e4 = hipFuncSetAttribute((const void*)asm_cols_4s, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)fs::lds_bytes(THZ_MAX_Z));
+    if (e4 != hipSuccess) err = e4;
   });
   if (err != hipSuccess) return fail(THZ_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s",
                                      hipGetErrorString(err));
@@ -1135,16 +1349,25 @@ static bool k2_pair(int Ph) {
   }();
   return on && Ph == 8192;
 }
+// Four-step K2 (asm_cols_4s) at Ph = 8192 for the analytic transfer function (ASM forward and
+// adjoint of one z-chunk); THZ_K2_4S=0 selects the three-stage asm_cols (A/B switch).
+static bool k2_4s(int Ph, const AsmArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K2_4S");
+    return !(e && e[0] == '0');
+  }();
+  return on && Ph == fs::N && !a.tft && !a.zsum;
+}
 static size_t k2_pair_lds(int Ph) {
   return (size_t)(2 * lds_floats2(Ph) + tw_lds_count(Ph)) * sizeof(float2) + 2 * 4 * THZ_MAX_Z;
 }
-static int k2_resident(int Ph, bool pair, int threads, size_t lds) {
+static int k2_resident(int Ph, bool pair, int threads, size_t lds, bool four = false) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, bool>, int> cache;
+  static std::map<std::tuple<int, int, bool, bool>, int> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_tuple(dev, Ph, pair);
+  auto key = std::make_tuple(dev, Ph, pair, four);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const void* k = nullptr;
@@ -1157,6 +1380,7 @@ static int k2_resident(int Ph, bool pair, int threads, size_t lds) {
     default: k = (const void*)asm_cols<0>; break;
   }
   if (mx_kind(Ph) == Mx300::N) k = (const void*)asm_cols_mx<Mx300>;
+  if (four) k = (const void*)asm_cols_4s;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1167,9 +1391,9 @@ static int k2_resident(int Ph, bool pair, int threads, size_t lds) {
 }
 
 // K2 task split: whole columns for the full dispatch rounds, the remainder split by z-range.
-static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds, bool pair = false) {
+static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds, bool pair = false, bool four = false) {
   const int nc = (pair ? (g.ncols + 1) / 2 : g.ncols) * g.BC;
-  const int G = k2_resident(g.Ph, pair, threads, lds);
+  const int G = k2_resident(g.Ph, pair, threads, lds, four);
   if (G <= 0 || a->nz <= 1) {
     a->kfull = nc;
     a->kparts = 1;
@@ -1282,6 +1506,11 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+      } else if (k2_4s(g.Ph, a)) {
+        // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
+        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z));
+        const int ntask = k2_tasks(g, &a, fs::T, lds2, false, true);
+        hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_pair(g.Ph)) {
         const size_t lds2 = k2_pair_lds(g.Ph);
         const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);

@@ -274,6 +274,8 @@ class _AsmLossFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, field, height, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
         ctx.set_materialize_grads(False)
+        if field.dtype != torch.complex64:  # thz_asm_forward_loss reads float2 pairs
+            raise TypeError(f"fused ASM loss computes in complex64 fields; got {field.dtype}")
         _require_device(field, "ASM")
         field = field.contiguous()
         B, C, H, W = field.shape

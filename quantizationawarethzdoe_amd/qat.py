@@ -252,7 +252,7 @@ class QATTrainer:
     """
 
     def __init__(self, system, target, lr=0.02, max_itrs=6000, group=None, graph=False, loss_fn=None,
-                 device_rng=True, capture_collective=False, force_collective=False):
+                 device_rng=True, capture_collective=False, force_collective=False, optimizer="adam"):
         self.system = system
         self.target = target.to(system.device).float().contiguous()
         self.max_itrs = max_itrs
@@ -260,9 +260,11 @@ class QATTrainer:
         # loss(out_field_data, target): the fused HIP |E|^2 -> normalize -> MSE by default
         self.loss_fn = loss_fn or _optics.intensity_mse
         params = list(system.parameters())
-        # one fused Adam kernel per step on the GPU (torch's multi-tensor path launches ~7 small kernels)
-        self.optimizer = torch.optim.Adam(params, lr=lr, capturable=graph,
-                                          fused=bool(params) and params[0].is_cuda)
+        # one fused Adam kernel per step on the GPU (torch's multi-tensor path launches ~7 small kernels).
+        # "adamw": the notebook's full-precision, naive-Gumbel and STE runs use torch.optim.AdamW with
+        # its defaults (weight_decay 0.01; experiment_four_focal_spots.ipynb cells 22, 33, 52)
+        opt = {"adam": torch.optim.Adam, "adamw": torch.optim.AdamW}[optimizer]
+        self.optimizer = opt(params, lr=lr, capturable=graph, fused=bool(params) and params[0].is_cuda)
         self.allreduce = GradientAllReduce(list(system.parameters()), group=group, force=force_collective)
         self.capture_collective = bool(capture_collective)
         self._one = torch.ones((), dtype=torch.float32, device=system.device)

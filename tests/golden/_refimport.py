@@ -63,4 +63,5 @@ def import_reference():
     ns.GB = importlib.import_module("LightSource.Gaussian_beam")
     ns.HF = importlib.import_module("utils.Helper_Functions")
     ns.import_module = importlib.import_module
+    ns.root = REF
     return ns

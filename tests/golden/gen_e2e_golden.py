@@ -7,16 +7,22 @@ target of define_FoM (nb :89-181) and its gradient with respect to the height ma
 SURVEY.md §8(c) procedure and fp32 as shipped.  This is the deterministic end-to-end golden of
 SURVEY §4 / §8(c): FixDOEElement(tolerance=0) -> ASM has no RNG in its output.
 
-The reference's own designed maps (edoe_4levels.npy, plot_data/example_1/splitter_*.npy) are
-numpy OBJECT arrays (pickled dicts written by DOE .save(), Components/QuantizedDOE.py:253-267):
-``np.load(..., allow_pickle=False)`` refuses them, and this build never unpickles files shipped
-with the reference, so they are not used.  Instead two maps are designed here the way a 4-level
-splitter is: the phase of the superposition of the tilted plane waves that focus on the target's
-spots at f = 200 mm, quantised to 4 levels of lambda / (4 (n - 1)) height:
+Cases:
 
-* ``splitter4_80``  -- 80 x 80 map (the notebooks' crop size), 4 spots at (+-20, +-20) mm; the
-  DOE upsamples it to the 100 x 100 field by nearest interpolation (QuantizedDOE.py:102-107);
-* ``splitter9_100`` -- 100 x 100 map, the target's 9 spots.
+* the REFERENCE's own trained maps (edoe_4levels.npy and plot_data/example_1/splitter_{ours, STE,
+  PSQ, GS, full_precision}.npy): the 80 x 80 centre crops that the notebook's
+  ``best_setup.doe.save(crop_size=[80, 80])`` wrote (experiment_four_focal_spots.ipynb cells 13, 29,
+  39, 48, 56; Components/QuantizedDOE.py:253-267).  The files are numpy OBJECT arrays (a pickled
+  dict); they are read by ``refdoe_parse.parse_pickled_npy``, a token parser that executes nothing
+  from the file (no pickle loader runs on them).  ``ref_<name>_pad100``: the crop zero-padded back
+  to the 100 x 100 DOE -- the system's 80 mm aperture (80 x 80 pixels) zeroes the field outside
+  the crop before the DOE, so this reproduces the trained DOE's detector field exactly;
+  ``ref_ours_80``: the 80 x 80 crop as a user would load it, upsampled by the FixDOE's nearest
+  interpolation (QuantizedDOE.py:102-107).
+* two maps designed here the way a 4-level splitter is: the phase of the superposition of the
+  tilted plane waves that focus on the target's spots at f = 200 mm, quantised to 4 levels of
+  lambda / (4 (n - 1)) height: ``splitter4_80`` (80 x 80, 4 spots at (+-20, +-20) mm, upsampled
+  to the 100 x 100 field) and ``splitter9_100`` (100 x 100, the target's 9 spots).
 
 Runs only in the build container (imports /root/reference through ``_refimport``)::
 
@@ -115,6 +121,19 @@ def main():
     torch.set_num_threads(8)
     lam32 = float(np.float32(C0 / F0))
     cases = {"splitter4_80": designed_map(80, FOCI4, lam32), "splitter9_100": designed_map(100, FOCI9, lam32)}
+    sources = {}
+    from refdoe_parse import parse_pickled_npy
+    refmaps = [("edoe_4levels", "edoe_4levels.npy")] + [
+        (n, f"plot_data/example_1/splitter_{n}.npy") for n in ("ours", "STE", "PSQ", "GS", "full_precision")]
+    for name, rel in refmaps:
+        d = parse_pickled_npy(os.path.join(ref.root, rel))
+        t = np.asarray(d["thickness"], dtype=np.float32)
+        assert t.shape == (80, 80) and abs(float(d["dxy"]) - 1e-3) < 1e-12
+        cases[f"ref_{name}_pad100"] = np.pad(t, 10)
+        sources[f"ref_{name}_pad100"] = rel
+        if name == "ours":
+            cases["ref_ours_80"] = t
+            sources["ref_ours_80"] = rel
     arrays, meta = {}, []
     for name, h in cases.items():
         arrays[f"{name}__h"] = h
@@ -130,8 +149,10 @@ def main():
             print(f"{name} fp{tag}: loss {r['loss']:.9e}", flush=True)
         o32, o64 = arrays[f"{name}__out32"], arrays[f"{name}__out64"]
         rel = float(np.linalg.norm(o32 - o64) / np.linalg.norm(o64))
-        meta.append(dict(name=name, shape=list(h.shape), levels=sorted(set(np.round(h.ravel() * 1e6).tolist())),
-                         rel32vs64=rel))
+        lv = sorted(set(np.round(h.ravel() * 1e6).tolist()))
+        meta.append(dict(name=name, shape=list(h.shape), levels=lv if len(lv) <= 8 else f"{len(lv)} distinct",
+                         rel32vs64=rel, source=sources.get(name, "designed here"),
+                         loss64=float(arrays[f"{name}__loss64"])))
         print(f"  {name}: reference fp32 vs fp64 field rel-L2 {rel:.2e}")
     np.savez_compressed(os.path.join(HERE, "e2e_golden.npz"), **arrays)
     with open(os.path.join(HERE, "e2e_manifest.json"), "w") as fh:

@@ -244,12 +244,50 @@ def test_asm_paired_column_kernel_bit_identical():
     code = _PAIR_SCRIPT.format(root=root)
     digests = []
     for flag in ("1", "0"):
-        env = dict(os.environ, THZ_K2_PAIR=flag)
+        env = dict(os.environ, THZ_K2_PAIR=flag, THZ_K2_4S="0")
         r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
                            timeout=180)
         assert r.returncode == 0, r.stderr[-2000:]
         digests.append(r.stdout.strip().splitlines()[-1])
     assert digests[0] == digests[1]
+
+
+_K2_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from tests.test_asm_gpu import _cfg2_input
+from quantizationawarethzdoe_amd.propagation import asm_apply
+x, lam = _cfg2_input(torch.device("cuda:0"))
+sp = [float(torch.tensor(0.25e-3, dtype=torch.float32))] * 2
+zs = [float(v) for v in torch.linspace(20e-3, 120e-3, 7, dtype=torch.float64)]
+out = asm_apply(x, [lam], sp, zs, 2048, 2048, True, 1)
+g = torch.randn(1, 1, 1, 4096, 4096, dtype=torch.complex64, device="cuda:0",
+                generator=torch.Generator(device="cuda:0").manual_seed(3))
+adj = asm_apply(g, [lam], sp, [0.07], 2048, 2048, True, 1, adjoint=True)
+np.save({path!r}, np.concatenate([out[:, 0, 0, ::4, ::4].cpu().numpy().reshape(-1),
+                                  adj.reshape(4096, 4096)[::4, ::4].cpu().numpy().reshape(-1)]))
+"""
+
+
+def test_asm_four_step_k2_matches_three_stage(tmp_path):
+    """The four-step column pass (asm_cols_4s, the default at Ph = 8192: eight 1024-point wavefront
+    transforms and one radix-8 step across the waves per z) against the three-stage asm_cols<8192>
+    (THZ_K2_4S=0) on the cfg2 geometry: 7 planes over 20-120 mm (the kparts z-range split of the
+    last dispatch round included) and one adjoint plane.  Same transform, other rounding order:
+    rel-L2 <= 2e-6 (fp32 FFT rounding of an 8192-point transform pair)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for flag in ("1", "0"):
+        path = str(tmp_path / f"k2_{flag}.npy")
+        env = dict(os.environ, THZ_K2_4S=flag)
+        r = subprocess.run([sys.executable, "-c", _K2_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(np.load(path))
+    assert rel_l2(res[0], res[1]) <= 2e-6
 
 
 def test_asm_p2048_64_planes_every_plane_vs_oracle():

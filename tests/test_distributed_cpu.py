@@ -176,20 +176,33 @@ def test_bench_refuses_gpus_world_mismatch():
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
 
 
-def test_bench_secondary_watchdog_prints_the_line_and_exits():
+def test_bench_secondary_watchdog_prints_the_line_and_exits_nonzero():
     """A secondary that hangs (e.g. in a collective) must not cost the headline line: the watchdog
-    prints the line with the finished secondaries and the rest marked as timed out, and exits 0."""
+    prints the line with the finished secondaries (the snapshot the main thread published) and the
+    rest marked as timed out, reports a finished secondary's failed output check on stderr, and
+    exits with WATCHDOG_EXIT (a hang is not a success)."""
     import json
     import subprocess
     import sys
     code = ("import json, time, bench\n"
-            "line = {'metric': 'm', 'value': 1.0, 'secondary': {}}\n"
-            "bench._secondary_watchdog(line, ['cfg3_czt', 'cfg4_qat'], 0, 0.5)\n"
-            "line['secondary']['cfg3_czt'] = {'value': 2.0}\n"
+            "line = {'metric': 'm', 'value': 1.0}\n"
+            "snap = [{}]\n"
+            "bench._secondary_watchdog(line, ['cfg3_czt', 'cfg4_qat'], 0, 0.5, snap)\n"
+            "snap[0] = {'cfg3_czt': {'value': 2.0, 'output_check': {'ok': False, 'why': 'x'}}}\n"
             "time.sleep(60)\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
-    assert r.returncode == 0, r.stderr
+    import bench
+    assert r.returncode == bench.WATCHDOG_EXIT != 0, r.stderr
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out["value"] == 1.0 and out["secondary"]["cfg3_czt"] == {"value": 2.0}
+    assert out["value"] == 1.0 and out["secondary"]["cfg3_czt"]["value"] == 2.0
     assert "timed out" in out["secondary"]["cfg4_qat"]["error"]
+    assert "output check FAILED" in r.stderr and "cfg3_czt" in r.stderr
+
+
+def test_bench_failed_checks_helper():
+    import bench
+    sec = {"a": {"output_check": {"ok": True}}, "b": {"error": "boom"},
+           "c": {"modes": {"x": {"output_check": {"ok": False}}, "y": {"output_check": {"ok": True}}}}}
+    f = bench._failed_checks(sec)
+    assert len(f) == 1 and f[0].startswith("c.modes.x:")

@@ -5,9 +5,13 @@ with the notebook's own import lines (experiment_four_focal_spots.ipynb:198-260)
 REFERENCE's own run of the same system (tests/golden/e2e_golden.npz, gen_e2e_golden.py, fp64 by
 the SURVEY §8(c) procedure).
 
-The reference's designed maps (edoe_4levels.npy, plot_data/example_1/splitter_*.npy) are pickled
-object arrays that are never unpickled here (gen_e2e_golden.py); the maps are designed 4-level
-splitters of the same kind (an 80 x 80 map upsampled to the 100 x 100 field, and a 100 x 100 one).
+Cases (tests/golden/e2e_manifest.json): the REFERENCE's own trained maps -- edoe_4levels.npy and
+plot_data/example_1/splitter_{ours, STE, PSQ, GS, full_precision}.npy, the 80 x 80 crops its
+notebook saved, read by a token parser that executes nothing from the file
+(tests/golden/refdoe_parse.py) -- zero-padded back to the 100 x 100 DOE (the 80 mm aperture
+zeroes the field outside the crop, so this is the trained DOE's detector field) and, for
+splitter_ours, upsampled from 80 x 80 as the FixDOE does; plus two splitters designed by the
+generator (an 80 x 80 map upsampled to the 100 x 100 field, and a 100 x 100 one).
 
 Tolerances: the field before the DOE and the detector field rel-L2 <= 1e-4 (SURVEY §8(c) ASM
 bound; the reference's own fp32 error here is 5e-5), the loss within 1e-4 relative, the height-map

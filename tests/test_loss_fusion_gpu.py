@@ -202,3 +202,30 @@ def test_loss_near_convergence_vs_fp64_oracle(fused):
     assert 1e-10 < rv < 1e-6, rv  # near convergence: the loss is ~1e-8 of the target's scale
     assert abs(lv - rv) <= 1e-2 * rv, (lv, rv)
     assert rel_l2(gx.cpu().numpy(), rg.numpy()) <= 1e-2
+
+
+@pytest.mark.parametrize("how", ["wavelength_f64", "data_c128"])
+def test_deferred_loss_refuses_complex128_like_the_unfused_path(how):
+    """A complex128 propagation (float64 wavelength tensor or complex128 data) under
+    deferred_output() must not reach the complex64 fused-loss kernel: field_intensity_mse raises the
+    TypeError the unfused intensity_mse raises for a complex128 field, and the
+    same system in complex64 runs."""
+    from quantizationawarethzdoe_amd import optics
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    from quantizationawarethzdoe_amd.propagation import deferred_output
+    dev = _dev()
+    x = torch.randn(1, 1, 64, 64, dtype=torch.complex64, device=dev)
+    lam = torch.tensor([C0 / 300e9], dtype=torch.float64 if how == "wavelength_f64" else torch.float32)
+    data = x.to(torch.complex128) if how == "data_c128" else x
+    prop = ASM_prop(z_distance=0.05, padding_scale=2, device=dev)
+    target = torch.rand(1, 1, 64, 64, device=dev)
+    f = ElectricField(data=data, wavelengths=lam, spacing=1e-3, device=dev)
+    with deferred_output():
+        out = prop(f)
+        with pytest.raises(TypeError, match="complex64"):
+            optics.field_intensity_mse(out, target)
+    f32 = ElectricField(data=x, wavelengths=lam.float(), spacing=1e-3, device=dev)
+    with deferred_output():
+        loss = optics.field_intensity_mse(prop(f32), target)
+    assert torch.isfinite(loss)
