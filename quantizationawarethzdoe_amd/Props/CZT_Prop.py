@@ -93,7 +93,8 @@ class CZT_prop(nn.Module):
             # slice b[W:W+1] is empty and it returns a [B, C, 1, 0] field (Props/CZT_Prop.py:206,211;
             # run here).  Every other power-of-two Bluestein length raises there, and the library
             # refuses it (THZ_E_ARG -> RuntimeError).
-            out = x.new_zeros(x.shape[0], x.shape[1], 1, 0)
+            # (kept in the autograd graph as the reference's slice is: a zero gradient flows back)
+            out = x.new_zeros(x.shape[0], x.shape[1], 1, 0) + 0 * x.sum((-2, -1), keepdim=True)[..., :0]
         else:
             out = _CztFunction.apply(x, tuple(field.wavelengths_host), tuple(sp), self._zh, outputHeight,
                                      outputWidth, odx, ody)

@@ -198,6 +198,68 @@ __device__ __forceinline__ float2 vrs_ez(float2 ex, float2 ey, float x, float y,
 
 template <int PN>
 __device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq);
+// The K1 input element s of row h of plane `plane` (s < Win): the field, or what the fused
+// loaders make of it -- the loss gradient of the adjoint of the fused loss, the DOE modulation
+// t_c(h + noise) (writing the noisy height map once), or the VRS Ez plane.
+struct RowSrc {
+  const AsmArgs& a;
+  const float2* in;
+  const float2* src;
+  int h, bc;
+  bool ez;
+  const float2 *sx, *sy;
+  float xh;
+  int hsrc;
+  float lam_c;
+  const float2* lg_row = nullptr;
+  const float* lg_t = nullptr;
+  float lg_m = 0.f, lg_S = 0.f, lg_g = 0.f;
+  int lg_am = -1;
+  __device__ __forceinline__ RowSrc(const AsmArgs& a_, const float2* in_, int plane, int h_) : a(a_), in(in_), h(h_) {
+    bc = plane % a.BC;
+    src = in + ((size_t)((a.zsum ? a.zoff * a.BC : 0) + plane) * a.Hin + h) * a.Win;
+    // VRS (Props/RSC_Prop.py:294-303): plane b = 2 is Ez = Ex x / r + Ey y / r on the unpadded
+    // grid linspace(-N dx/2, N dx/2, N) (dx on both axes, :83-84)
+    ez = a.vec && bc / a.C == 2;
+    sx = in + ((size_t)(bc % a.C) * a.Hin + h) * a.Win;
+    sy = in + ((size_t)(a.C + bc % a.C) * a.Hin + h) * a.Win;
+    xh = ez ? lin(-(float)a.Hin * a.dx / 2.0f, (float)a.Hin * a.dx / 2.0f, a.Hin, h) : 0.f;
+    hsrc = a.mod_h ? doe_nearest_src(h, a.mod_hs, a.Hin) * a.mod_ws : 0;
+    lam_c = a.lam[bc % a.C];
+    // loss gradient rows: field E, target T and the statistics of batch item b
+    if (a.lg_field) {
+      const int b = bc / a.C, c = bc - b * a.C;
+      lg_row = a.lg_field + ((size_t)bc * a.Hin + h) * a.Win;
+      const int tb = a.lg_tB == 1 ? 0 : b, tc = a.lg_tC == 1 ? 0 : c;
+      lg_t = a.lg_target + (((size_t)tb * a.lg_tC + tc) * a.Hin + h) * a.Win;
+      lg_m = a.lg_stats[3 * b];
+      lg_S = a.lg_stats[3 * b + 2];
+      // the argmax relative to this row's first element (c H + h) W
+      lg_am = __float_as_int(a.lg_stats[3 * b + 1]) - (c * a.Hin + h) * a.Win;
+      lg_g = a.lg_gloss[0] * a.lg_two_inv_n;
+    }
+  }
+  __device__ __forceinline__ float2 operator()(int s) const {
+    if (a.lg_field) {  // dL/dE = 2 E dL/dI, dL/dI = g (r / m - [argmax] S / m^2) (mse_backward_kernel)
+      const float2 e = lg_row[s];
+      const float I = loss_intensity(e);
+      const float r = I / lg_m - lg_t[s];
+      float dI = lg_g * r / lg_m;
+      if (s == lg_am) dI -= lg_g * lg_S / (lg_m * lg_m);
+      const float2 gl = make_float2(2.f * dI * e.x, 2.f * dI * e.y);
+      return in ? cadd(src[s], gl) : gl;
+    }
+    if (a.mod_h) {  // DOELayer.modulate fused into the loader (Components/QuantizedDOE.py:92-126)
+      const float hv = doe_noisy_h(a.mod_h, a.mod_u, hsrc + doe_nearest_src(s, a.mod_ws, a.Win), a.mod_tol,
+                                   a.mod_rng, a.mod_rng_stream);
+      if (a.mod_hfull && bc == 0) a.mod_hfull[(size_t)h * a.Win + s] = hv;
+      return cmul(src[s], doe_transmission(hv, lam_c, a.mod_eps, a.mod_tand, nullptr));
+    }
+    if (!ez) return src[s];
+    return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
+  }
+};
+
 
 template <int PN>
 __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
@@ -217,52 +279,8 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
   // plane = zz * BC + bc: one plane (zz = 0) except in the Z-summing adjoint, whose chunk's input
   // planes start at plane zoff * BC of `in`
   const int plane = row / a.Hin, h = row - plane * a.Hin;
-  const int bc = plane % a.BC;
-  const float2* src = in + ((size_t)((a.zsum ? a.zoff * a.BC : 0) + plane) * a.Hin + h) * a.Win;
   float2* dst = T + (size_t)plane * a.ncb * CB * a.Hin;
-  // VRS (Props/RSC_Prop.py:294-303): plane b = 2 is Ez = Ex x / r + Ey y / r on the unpadded
-  // grid linspace(-N dx/2, N dx/2, N) (dx on both axes, :83-84)
-  const bool ez = a.vec && bc / a.C == 2;
-  const float2* sx = in + ((size_t)(bc % a.C) * a.Hin + h) * a.Win;
-  const float2* sy = in + ((size_t)(a.C + bc % a.C) * a.Hin + h) * a.Win;
-  const float xh = ez ? lin(-(float)a.Hin * a.dx / 2.0f, (float)a.Hin * a.dx / 2.0f, a.Hin, h) : 0.f;
-  const int hsrc = a.mod_h ? doe_nearest_src(h, a.mod_hs, a.Hin) * a.mod_ws : 0;
-  const float lam_c = a.lam[bc % a.C];
-  // loss gradient rows: field E, target T and the statistics of batch item b
-  const float2* lg_row = nullptr;
-  const float* lg_t = nullptr;
-  float lg_m = 0.f, lg_S = 0.f, lg_g = 0.f;
-  int lg_am = -1;
-  if (a.lg_field) {
-    const int b = bc / a.C, c = bc - b * a.C;
-    lg_row = a.lg_field + ((size_t)bc * a.Hin + h) * a.Win;
-    const int tb = a.lg_tB == 1 ? 0 : b, tc = a.lg_tC == 1 ? 0 : c;
-    lg_t = a.lg_target + (((size_t)tb * a.lg_tC + tc) * a.Hin + h) * a.Win;
-    lg_m = a.lg_stats[3 * b];
-    lg_S = a.lg_stats[3 * b + 2];
-    // the argmax relative to this row's first element (c H + h) W
-    lg_am = __float_as_int(a.lg_stats[3 * b + 1]) - (c * a.Hin + h) * a.Win;
-    lg_g = a.lg_gloss[0] * a.lg_two_inv_n;
-  }
-  auto fetch = [&](int s) {
-    if (a.lg_field) {  // dL/dE = 2 E dL/dI, dL/dI = g (r / m - [argmax] S / m^2) (mse_backward_kernel)
-      const float2 e = lg_row[s];
-      const float I = loss_intensity(e);
-      const float r = I / lg_m - lg_t[s];
-      float dI = lg_g * r / lg_m;
-      if (s == lg_am) dI -= lg_g * lg_S / (lg_m * lg_m);
-      const float2 gl = make_float2(2.f * dI * e.x, 2.f * dI * e.y);
-      return in ? cadd(src[s], gl) : gl;
-    }
-    if (a.mod_h) {  // DOELayer.modulate fused into the loader (Components/QuantizedDOE.py:92-126)
-      const float hv = doe_noisy_h(a.mod_h, a.mod_u, hsrc + doe_nearest_src(s, a.mod_ws, a.Win), a.mod_tol,
-                                   a.mod_rng, a.mod_rng_stream);
-      if (a.mod_hfull && bc == 0) a.mod_hfull[(size_t)h * a.Win + s] = hv;
-      return cmul(src[s], doe_transmission(hv, lam_c, a.mod_eps, a.mod_tand, nullptr));
-    }
-    if (!ez) return src[s];
-    return vrs_ez(sx[s], sy[s], xh, lin(-(float)a.Win * a.dx / 2.0f, (float)a.Win * a.dx / 2.0f, a.Win, s), a.zr);
-  };
+  const RowSrc fetch(a, in, plane, h);
   if constexpr (PN > 0 && !is_mx(PN)) {
     // twiddle-table loads first, their LDS writes after the row loads (as in K3)
     constexpr int TT = Geo<PN>::T;
@@ -978,6 +996,323 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
   asm_cols_mx_body<MP, false>(T, U, ph, a);
 }
 
+// ---------------------------------------------------------------------------------------------
+// K2 at Ph = 300 with the input and output windows both [100, 200) (the cfg4 / cfg5 layers:
+// 100-row fields, padding_scale 2, cropped output): the 300-point column transforms split into
+// three 100-point ones.  With W = exp(-2 pi i / 300) and k = 3 k' + r (r < 3), the forward of the
+// window x'[n'] = x[100 + n'] is
+//   X[3 k' + r] = w3^r DFT_100(x'[n'] W^(r n'))[k'],
+// and the inverse kept rows y[100 + m'] = sum_r w3^-r W^(-r m') IDFT_100(Y[3 k' + r])[m'] -- the
+// w3^(+-r) of one class cancel (Y = X H class by class).  So per column and class r: a pre-twiddle,
+// a 100-point forward, x H_z, a 100-point inverse, a post-twiddle, and a sum over the classes:
+// about 20 % less arithmetic than the padded 300-point pair, and the 100-point transforms run as
+// 10 x 10 (prime-factor radix 10, no inner twiddles) on 60 of the 64 lanes -- two columns per wave,
+// lane = 32 half + 10 r + i -- where the 5 3 4 5 plan keeps 60/100/75/60 butterflies on 64 lanes.
+// Spectrum, sqrt(k^2 - K^2) and bounds as asm_cols_mx (per-column tables); the Z loop keeps the
+// spectrum in registers.  The LDS image of class (half, r) is 100 elements at stride M3_IMS
+// (bank-model search, /tmp-free: both exchanges and the class sum within 1.5x of conflict-free).
+constexpr int M3_L = 100;
+constexpr int M3_IMS = 107;
+constexpr size_t m3_lds_bytes() { return (size_t)6 * M3_IMS * sizeof(float2); }
+
+// 10-point DFT, prime-factor 2 x 5 (no twiddles): input j = (5 j1 + 2 j2) mod 10, output
+// q = (5 q1 + 6 q2) mod 10
+template <bool INV>
+__device__ __forceinline__ void dft10(float2* v) {
+  float2 a[5], b[5];
+#pragma unroll
+  for (int j2 = 0; j2 < 5; ++j2) {
+    a[j2] = v[(2 * j2) % 10];
+    b[j2] = v[(5 + 2 * j2) % 10];
+  }
+  dft5<INV>(a);
+  dft5<INV>(b);
+#pragma unroll
+  for (int q2 = 0; q2 < 5; ++q2) {
+    v[(6 * q2) % 10] = cadd(a[q2], b[q2]);
+    v[(5 + 6 * q2) % 10] = csub(a[q2], b[q2]);
+  }
+}
+
+// ONEZ: one z-plane per launch (the layers' case): the spectrum is consumed in place by the
+// transfer-function product instead of being held across a z loop (20 registers fewer: 8 waves /
+// SIMD without spills; the Z-loop form runs at 5)
+template <bool ONEZ>
+__device__ __forceinline__ void asm_cols_m3_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                 const AsmArgs& a) {
+  constexpr int PN = 3 * M3_L;
+  extern __shared__ float2 lds[];
+  int id, z_lo = 0, z_hi = a.nz;
+  if ((int)blockIdx.x < a.kfull) {
+    id = xcd_chunk(blockIdx.x, a.kfull);
+  } else {
+    const int t = blockIdx.x - a.kfull, part = t % a.kparts;
+    id = a.kfull + t / a.kparts;
+    z_lo = part * a.nz / a.kparts;
+    z_hi = (part + 1) * a.nz / a.kparts;
+  }
+  const int npair = (a.ncols + 1) / 2;
+  const int bc = id / npair, pr = id - bc * npair;
+  const int lane = threadIdx.x, h = lane >> 5, rem = lane & 31;
+  const bool act = rem < 30;                        // lanes 30, 31 of each half idle
+  const int r = act ? rem / 10 : 0, i = act ? rem - 10 * r : 0;
+  int c = 2 * pr + h;
+  if (c >= a.ncols) c = a.ncols - 1;                // the odd last column's partner half: no stores
+  const float2* __restrict__ tw = ph.tw;           // W^t, t < 300
+  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
+  float2* img = lds + (3 * h + r) * M3_IMS;
+  // forward, class r: x'[i + 10 j] W^(r (i + 10 j)), radix 10 over j, then over i
+  float2 F[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const int n = i + 10 * j;
+    const float2 x = col[(size_t)n * CB];
+    F[j] = r ? cmul(x, tw[r * n]) : x;
+  }
+  dft10<false>(F);
+  if (act) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) img[10 * i + q] = F[q];
+  }
+  wf::wave_sync();
+#pragma unroll
+  for (int j = 0; j < 10; ++j) F[j] = img[i + 10 * j];
+#pragma unroll
+  for (int j = 1; j < 10; ++j) F[j] = cmul(F[j], tw[3 * i * j]);
+  dft10<false>(F);  // F[q] = X_r[i + 10 q] (w3^r dropped, see above)
+  // spectrum element q is k = 3 (i + 10 q) + r
+  const size_t tc = (size_t)(bc % a.C) * a.ncols + c;
+  const int* mzc = a.mzt + tc * a.nz;
+  const float* sqc = a.sqt + tc * PN;
+  for (int zz = z_lo; zz < z_hi; ++zz) {
+    const float z = a.zv[a.zoff + zz];
+    const int M = mzc[zz];
+    int ii = i;
+    asm volatile("" : "+v"(ii));
+    float2 gz[10];
+    float2 (&g)[10] = ONEZ ? F : gz;
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const int k = 3 * (ii + 10 * q) + r;
+      const int mx = freq_index(k, PN);
+      if (mx > M || -mx > M) {
+        g[q] = make_float2(0.f, 0.f);
+        continue;
+      }
+      // sqrt(k^2 - K^2) read per z from the column table (L2-resident; the layers run one z, and ten
+      // registers held across the loop push the kernel below 8 waves / SIMD)
+      float sn, cs;
+      sincos_hw(tf_mul(z, sqc[k]), &sn, &cs);
+      g[q] = cmul(F[q], make_float2(cs, a.adjoint ? -sn : sn));
+    }
+    // inverse, class r: radix 10 over q (inputs k' = i + 10 q), then over i
+    dft10<true>(g);
+    wf::wave_sync();  // the previous z's class-sum reads of the images are done
+    if (act) {
+#pragma unroll
+      for (int q = 0; q < 10; ++q) img[10 * ii + q] = g[q];
+    }
+    wf::wave_sync();
+#pragma unroll
+    for (int j = 0; j < 10; ++j) g[j] = img[ii + 10 * j];
+    {
+      // w100^(i j) by products of w100^i (one table load; the 19 loads of direct lookups would be
+      // issued together and held in registers)
+      const float2 w1 = tw[3 * ii];
+      float2 wj = w1;
+#pragma unroll
+      for (int j = 1; j < 10; ++j) {
+        g[j] = cmulc(g[j], wj);
+        if (j < 9) wj = cmul(wj, w1);
+      }
+    }
+    dft10<true>(g);  // g[q] = IDFT_100(Y_r)[m'], m' = i + 10 q
+    wf::wave_sync();
+    if (act) {
+      // W^(r m') = W^(r i) (W^(10 r))^q
+      const float2 st = tw[10 * r];
+      float2 wq = tw[r * ii];
+#pragma unroll
+      for (int q = 0; q < 10; ++q) {
+        img[ii + 10 * q] = cmulc(g[q], wq);
+        if (q < 9) wq = cmul(wq, st);
+      }
+    }
+    wf::wave_sync();
+    // the class sum of the 2 x 100 kept rows: output o = lane + 64 t
+    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int o = lane + 64 * t;
+      if (o >= 2 * M3_L) continue;
+      const int hh = o >= M3_L, m = o - M3_L * hh;
+      const int cc = 2 * pr + hh;
+      const float2* s0 = lds + 3 * hh * M3_IMS + m;
+      const float2 v = cadd(cadd(s0[0], s0[M3_IMS]), s0[2 * M3_IMS]);
+      if (cc < a.ncols) dst[blk_u(cc, m, a.Hout)] = cscale(v, a.scale);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8)))
+asm_cols_m3(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_m3_body<true>(T, U, ph, a);
+}
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
+asm_cols_m3_z(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_m3_body<false>(T, U, ph, a);
+}
+
+// The row passes of the same geometry (Pw = 300, input columns [100, 200) for K1, output columns
+// [100, 200) for K3) on the same 3 x 100 split, two rows per wave (lane = 32 half + 10 r + i).
+// K1: the 100 inputs of a row are formed once (lane e of the half takes elements e + 30 t: the fused
+// DOE modulation / loss-gradient loaders run once per element) and staged in LDS, then each class
+// r runs its pre-twiddle and 100-point forward, storing the band columns of k = 3 k' + r.
+// K3: each class gathers its band columns k = 3 k' + r, runs the 100-point inverse and its
+// post-twiddle; the class sum gives the 100 kept outputs of the row.
+constexpr size_t m3_rows_fwd_lds_bytes() { return (size_t)(2 * M3_L + 6 * M3_IMS) * sizeof(float2); }
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8)))
+asm_rows_fwd_m3(const float2* __restrict__ in, float2* __restrict__ T, FftPlan pw, AsmArgs a) {
+  constexpr int PN = 3 * M3_L;
+  extern __shared__ float2 lds[];
+  const int nblk = gridDim.x - a.tab_blocks;
+  if ((int)blockIdx.x >= nblk) {  // the column pass's tables of the first z-chunk, as asm_rows_fwd
+    tf_tables_body<PN>(a, blockIdx.x - nblk, 1);
+    return;
+  }
+  const int rows = (a.zsum ? a.nz : 1) * a.BC * a.Hin;
+  const int lane = threadIdx.x, h = lane >> 5, rem = lane & 31;
+  const bool act = rem < 30;
+  const int r = act ? rem / 10 : 0, i = act ? rem - 10 * r : 0;
+  const int row = 2 * (int)blockIdx.x + h;
+  const bool live = row < rows;
+  const int rw = live ? row : rows - 1;
+  const int plane = rw / a.Hin, hr = rw - plane * a.Hin;
+  const RowSrc fetch(a, in, plane, hr);
+  float2* rowbuf = lds + h * M3_L;
+  if (live && act) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int e = rem + 30 * t;
+      if (e < M3_L) rowbuf[e] = fetch(e);
+    }
+  }
+  wf::wave_sync();
+  const float2* __restrict__ tw = pw.tw;
+  float2 F[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const int n = i + 10 * j;
+    const float2 x = rowbuf[n];
+    F[j] = r ? cmul(x, tw[r * n]) : x;
+  }
+  dft10<false>(F);
+  float2* img = lds + 2 * M3_L + (3 * h + r) * M3_IMS;
+  if (act) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) img[10 * i + q] = F[q];
+  }
+  wf::wave_sync();
+#pragma unroll
+  for (int j = 0; j < 10; ++j) F[j] = img[i + 10 * j];
+#pragma unroll
+  for (int j = 1; j < 10; ++j) F[j] = cmul(F[j], tw[3 * i * j]);
+  dft10<false>(F);  // X[3 (i + 10 q) + r] = w3^r F[q]
+  if (!(live && act)) return;
+  const float2 w3r = r ? tw[M3_L * r] : make_float2(1.f, 0.f);  // w3^r = W^(100 r)
+  float2* dst = T + (size_t)plane * a.ncb * CB * a.Hin;
+#pragma unroll
+  for (int q = 0; q < 10; ++q) {
+    const int c = band_col(3 * (i + 10 * q) + r, PN, a.J, a.ncols);
+    if (c >= 0) dst[blk(c, hr, a.Hin)] = r ? cmul(F[q], w3r) : F[q];
+  }
+}
+
+template <bool LOSS>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8)))
+asm_rows_inv_m3(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw, AsmArgs a) {
+  constexpr int PN = 3 * M3_L;
+  extern __shared__ float2 lds[];
+  const int rows = a.nz * a.BC * a.Hout;
+  const int lane = threadIdx.x, h = lane >> 5, rem = lane & 31;
+  const bool act = rem < 30;
+  const int r = act ? rem / 10 : 0, i = act ? rem - 10 * r : 0;
+  const int row = 2 * (int)blockIdx.x + h;
+  const int rw = row < rows ? row : rows - 1;
+  const int plane = rw / a.Hout, ro = rw - plane * a.Hout;
+  const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
+  const float2* __restrict__ tw = pw.tw;
+  // class r: Y[3 (i + 10 j) + r] (zero outside the band), the w3^-r of the class folded in
+  float2 g[10];
+#pragma unroll
+  for (int j = 0; j < 10; ++j) {
+    const int c = band_col(3 * (i + 10 * j) + r, PN, a.J, a.ncols);
+    g[j] = c >= 0 ? src[blk_u(c, ro, a.Hout)] : make_float2(0.f, 0.f);
+  }
+  dft10<true>(g);
+  float2* img = lds + (3 * h + r) * M3_IMS;
+  if (act) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) img[10 * i + q] = g[q];
+  }
+  wf::wave_sync();
+#pragma unroll
+  for (int j = 0; j < 10; ++j) g[j] = img[i + 10 * j];
+  {
+    const float2 w1 = tw[3 * i];
+    float2 wj = w1;
+#pragma unroll
+    for (int j = 1; j < 10; ++j) {
+      g[j] = cmulc(g[j], wj);
+      if (j < 9) wj = cmul(wj, w1);
+    }
+  }
+  dft10<true>(g);  // IDFT_100 of the class, m' = i + 10 q
+  wf::wave_sync();
+  if (act) {
+    // w3^-r W^(-r m') = W^(-r (100 + m')): one table entry and its steps W^(-10 r)
+    const float2 st = tw[10 * r];
+    float2 wq = tw[r * (M3_L + i)];
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      img[i + 10 * q] = cmulc(g[q], wq);
+      if (q < 9) wq = cmul(wq, st);
+    }
+  }
+  wf::wave_sync();
+  // the class sum of the 2 x 100 outputs: output o = lane + 64 t (row o / 100)
+  LossAcc acc[2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int o = lane + 64 * t;
+    if (o >= 2 * M3_L) continue;
+    const int hh = o >= M3_L, w = o - M3_L * hh;
+    const int rr = 2 * (int)blockIdx.x + hh;
+    if (rr >= rows) continue;
+    const int pl = rr / a.Hout, rout = rr - pl * a.Hout;
+    const float2* s0 = lds + 3 * hh * M3_IMS + w;
+    const float2 v = cadd(cadd(s0[0], s0[M3_IMS]), s0[2 * M3_IMS]);  // (1 / (Ph Pw) applied by K2)
+    out[((size_t)(a.zoff * a.BC + pl) * a.Hout + rout) * a.Wout + w] = v;
+    if constexpr (LOSS) {
+      const int lb = pl / a.C, lc = pl - lb * a.C;
+      const int tb = a.ls.tB == 1 ? 0 : lb, tc = a.ls.tC == 1 ? 0 : lc;
+      const float tv = a.ls.target[(((size_t)tb * a.ls.tC + tc) * a.Hout + rout) * a.Wout + w];
+      acc[hh].add(v, tv, (unsigned)((lc * a.Hout + rout) * a.Wout + w));
+    }
+  }
+  if constexpr (LOSS) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int rr = 2 * (int)blockIdx.x + hh;
+      if (rr >= rows) continue;  // uniform over the workgroup
+      const int pl = rr / a.Hout, rout = rr - pl * a.Hout;
+      const int lb = pl / a.C, lc = pl - lb * a.C;
+      loss_store_part(acc[hh], a.ls, lb, lc * a.Hout + rout);  // the slot of asm_rows_inv_loss
+    }
+  }
+}
+
 template <class MP>
 __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_zsum(
     const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
@@ -1358,16 +1693,34 @@ static bool k2_4s(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == fs::N && !a.tft && !a.zsum;
 }
+// The 3 x 100 row passes (asm_rows_fwd_m3 / asm_rows_inv_m3) at Pw = 300 with the input (K1) or
+// output (K3) columns [100, 200); THZ_K2_M3=0 selects the 5 3 4 5 row kernels too.
+static bool m3_on() {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K2_M3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool k1_m3(int Pw, const AsmArgs& a) { return m3_on() && Pw == 3 * M3_L && a.in_c0 == M3_L && a.Win == M3_L; }
+static bool k3_m3(int Pw, const AsmArgs& a) { return m3_on() && Pw == 3 * M3_L && a.out_c0 == M3_L && a.Wout == M3_L; }
+
+// The 3 x 100 column pass (asm_cols_m3) at Ph = 300 with both windows [100, 200) (cfg4 / cfg5
+// layers), analytic transfer function; THZ_K2_M3=0 selects the 5 3 4 5 asm_cols_mx (A/B switch).
+static bool k2_m3(int Ph, const AsmArgs& a) {
+  return m3_on() && Ph == 3 * M3_L && !a.tft && !a.zsum && a.in_r0 == M3_L && a.Hin == M3_L && a.out_r0 == M3_L &&
+         a.Hout == M3_L;
+}
 static size_t k2_pair_lds(int Ph) {
   return (size_t)(2 * lds_floats2(Ph) + tw_lds_count(Ph)) * sizeof(float2) + 2 * 4 * THZ_MAX_Z;
 }
-static int k2_resident(int Ph, bool pair, int threads, size_t lds, bool four = false) {
+static int k2_resident(int Ph, bool pair, int threads, size_t lds, const void* kern = nullptr) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, bool, bool>, int> cache;
+  static std::map<std::tuple<int, int, bool, const void*>, int> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_tuple(dev, Ph, pair, four);
+  auto key = std::make_tuple(dev, Ph, pair, kern);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const void* k = nullptr;
@@ -1380,7 +1733,7 @@ static int k2_resident(int Ph, bool pair, int threads, size_t lds, bool four = f
     default: k = (const void*)asm_cols<0>; break;
   }
   if (mx_kind(Ph) == Mx300::N) k = (const void*)asm_cols_mx<Mx300>;
-  if (four) k = (const void*)asm_cols_4s;
+  if (kern) k = kern;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1391,9 +1744,12 @@ static int k2_resident(int Ph, bool pair, int threads, size_t lds, bool four = f
 }
 
 // K2 task split: whole columns for the full dispatch rounds, the remainder split by z-range.
-static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds, bool pair = false, bool four = false) {
+// pair: two columns per task (asm_cols_pair, asm_cols_m3); kern: the kernel, when not the default
+// of its size
+static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds, bool pair = false,
+                    const void* kern = nullptr) {
   const int nc = (pair ? (g.ncols + 1) / 2 : g.ncols) * g.BC;
-  const int G = k2_resident(g.Ph, pair, threads, lds, four);
+  const int G = k2_resident(g.Ph, pair, threads, lds, kern);
   if (G <= 0 || a->nz <= 1) {
     a->kfull = nc;
     a->kparts = 1;
@@ -1433,8 +1789,13 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
     a.zacc = z0 > 0;
     {
       KernelTimer kt("asm_rows_fwd", s);
-      THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(a.nz * g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in, T,
-                      pw, a);
+      if (k1_m3(g.Pw, a)) {
+        hipLaunchKernelGGL(asm_rows_fwd_m3, dim3((a.nz * g.BC * g.Hin + 1) / 2), dim3(64), m3_rows_fwd_lds_bytes(), s,
+                           (const float2*)in, T, pw, a);
+      } else {
+        THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(a.nz * g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in,
+                        T, pw, a);
+      }
       THZ_LAUNCH_CHECK();
       kt.stop();
     }
@@ -1459,8 +1820,13 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
   a.nz = 1;
   {
     KernelTimer kt("asm_rows_inv", s);
-    THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
-                    (float2*)out, pw, a);
+    if (k3_m3(g.Pw, a)) {
+      hipLaunchKernelGGL(asm_rows_inv_m3<false>, dim3((g.BC * g.Hout + 1) / 2), dim3(64), m3_lds_bytes(), s,
+                         (const float2*)U, (float2*)out, pw, a);
+    } else {
+      THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
+                      (float2*)out, pw, a);
+    }
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
@@ -1486,8 +1852,13 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     KernelTimer kt("asm_rows_fwd", s);
     a.zoff = 0;
     a.nz = std::min(g.zc, Z);
-    THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin + a.tab_blocks), fft_lds_bytes_io(g.Pw), s,
-                    (const float2*)in, T, pw, a);
+    if (k1_m3(g.Pw, a)) {
+      hipLaunchKernelGGL(asm_rows_fwd_m3, dim3((g.BC * g.Hin + 1) / 2 + a.tab_blocks), dim3(64),
+                         m3_rows_fwd_lds_bytes(), s, (const float2*)in, T, pw, a);
+    } else {
+      THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin + a.tab_blocks), fft_lds_bytes_io(g.Pw), s,
+                      (const float2*)in, T, pw, a);
+    }
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
@@ -1502,14 +1873,21 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
           THZ_LAUNCH_CHECK();
         }
       }
-      if (mx_kind(g.Ph) == Mx300::N) {
+      if (k2_m3(g.Ph, a)) {
+        const void* kern = a.nz == 1 ? (const void*)asm_cols_m3 : (const void*)asm_cols_m3_z;
+        const int ntask = k2_tasks(g, &a, 64, m3_lds_bytes(), true, kern);
+        if (a.nz == 1)
+          hipLaunchKernelGGL(asm_cols_m3, dim3(ntask), dim3(64), m3_lds_bytes(), s, (const float2*)T, U, ph, a);
+        else
+          hipLaunchKernelGGL(asm_cols_m3_z, dim3(ntask), dim3(64), m3_lds_bytes(), s, (const float2*)T, U, ph, a);
+      } else if (mx_kind(g.Ph) == Mx300::N) {
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_4s(g.Ph, a)) {
         // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
         const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z));
-        const int ntask = k2_tasks(g, &a, fs::T, lds2, false, true);
+        const int ntask = k2_tasks(g, &a, fs::T, lds2, false, (const void*)asm_cols_4s);
         hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_pair(g.Ph)) {
         const size_t lds2 = k2_pair_lds(g.Ph);
@@ -1525,11 +1903,21 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     }
     {
       KernelTimer kt("asm_rows_inv", s);
+      const bool m3 = k3_m3(g.Pw, a);
+      const dim3 g3((a.nz * g.BC * g.Hout + 1) / 2);
       if (a.ls.stats) {
-        THZ_ROWS_SWITCH(g.Pw, asm_rows_inv_loss, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s,
-                        (const float2*)U, (float2*)out, pw, a);
+        if (m3) {
+          hipLaunchKernelGGL(asm_rows_inv_m3<true>, g3, dim3(64), m3_lds_bytes(), s, (const float2*)U, (float2*)out,
+                             pw, a);
+        } else {
+          THZ_ROWS_SWITCH(g.Pw, asm_rows_inv_loss, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s,
+                          (const float2*)U, (float2*)out, pw, a);
+        }
         THZ_LAUNCH_CHECK();
         if ((e = launch_loss_finish(a.ls, s))) return e;
+      } else if (m3) {
+        hipLaunchKernelGGL(asm_rows_inv_m3<false>, g3, dim3(64), m3_lds_bytes(), s, (const float2*)U, (float2*)out, pw,
+                           a);
       } else {
         THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
                         (float2*)out, pw, a);

@@ -258,7 +258,6 @@ __global__ void __launch_bounds__(1024) czt_cols(const float2* __restrict__ V, f
 constexpr int CZB_BS = wf::N / 2;
 
 constexpr int CZB_W = 8;   // rows pass: lines (waves) per workgroup (8: the twiddle tables are gathered once per 8 lines; 4 -> 8 measured 0.59 -> 0.565 ms at cfg3, profiles/r03_czt_probe.txt)
-constexpr int CZB_WC = CB;  // columns pass: one 16-column block of V per workgroup
 #ifndef CZB_WPE
 #define CZB_WPE 4
 #endif
@@ -351,30 +350,47 @@ __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu
 }
 
 // pass B (columns, H axis) of V -> out [BC][outW][outH]: out[p][q] = F0 * U * z dxo dyo lambda.
-// One workgroup per 16-column block of V (one wave per column).  A block's CZB_BS rows of the 16
-// columns are one contiguous 64 KiB run of V: the workgroup loads it coalesced (16 B per lane) and
-// transposes it through LDS, so each wave reads its column from LDS instead of one 8-byte
-// element per 128-byte line from L2.
-constexpr int CZB_TP = CZB_BS + 1;  // LDS tile row (one column): +1 element spreads the banks
-constexpr size_t czb_cols_lds_bytes() { return czb_lds_bytes(CZB_WC) + (size_t)CZB_WC * CZB_TP * sizeof(float2); }
+// One workgroup per half of a 16-column block of V (8 columns, one wave per column).  A block's
+// CZB_BS rows of the 8 columns are 512 rows x 64 B of V: the workgroup loads them coalesced (16 B
+// per lane) and writes each value straight into the image of the wave that transforms its column
+// (real parts at [0, 512), imaginary parts at [544, 1056): the first stage reads lane + 64 r, then
+// the transform's own exchanges reuse the image), so there is no separate transpose tile.  The
+// 53 KB of LDS per workgroup leave room for two workgroups per CU (VGPR-bound at 4 waves / SIMD):
+// one workgroup's block loads overlap the other's transforms.  (The round-3 form staged a whole
+// 16-column block through a 64 KB tile: one 16-wave workgroup per CU, every block load exposed.)
+// The sibling half-blocks of a V block run on one XCD (blockIdx b and b ^ 8), so the L2 merges
+// their half-line reads.
+constexpr int CZB_WC = CB / 2;  // columns pass: 8 columns (waves) per workgroup
+constexpr int CZB_IMS = wf::IMG + 4;  // wave image stride: +4 floats skews the images' banks for the block writes
+constexpr int CZB_IMM = 544;          // imaginary parts of the staged column, float offset in the image
+constexpr size_t czb_cols_lds_bytes() { return wf::TAB * sizeof(float2) + CZB_WC * CZB_IMS * sizeof(float); }
 
 template <bool PARTIAL>
 __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_cols_blk(const float2* __restrict__ V, float2* __restrict__ out,
                                                            const float2* __restrict__ ws, CztArgs a) {
-  static_assert(CZB_WC == CB, "one workgroup per V column block");
+  static_assert(2 * CZB_WC == CB, "two workgroups per V column block");
+  static_assert(CZB_IMM + CZB_BS <= wf::IMG && CZB_IMM % 32 == 0, "staged column inside the wave image");
   extern __shared__ float2 lds[];
-  const wf::Tabs tw = wf::fill_tables(lds, a.tw1024, threadIdx.x, blockDim.x);
-  float* img = wf::wave_image(lds, threadIdx.x >> 6);
-  float2* tile = reinterpret_cast<float2*>(reinterpret_cast<float*>(lds + wf::TAB) + CZB_WC * wf::IMG);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int bc = blockIdx.x / a.ncbA, qb = blockIdx.x - bc * a.ncbA;
-  const int q = qb * CZB_WC + wave;
-  const bool live = q < a.outH;  // every wave takes part in the tile loads and barriers
+  float* const img0 = reinterpret_cast<float*>(lds + wf::TAB);
+  float* img = img0 + wave * CZB_IMS;
+  {
+    int off = 0;
+    asm volatile("" : "+v"(off));  // keep the image base in the address register (wf::wave_image)
+    img += off;
+  }
+  // blockIdx -> (block, half): halves h = 0, 1 of block id at blockIdx (id & 7) | ((id >> 3) << 4) | (h << 3)
+  const int bid = (int)blockIdx.x, hb = (bid >> 3) & 1, blkid = (bid & 7) | ((bid >> 4) << 3);
+  if (blkid >= a.BC * a.ncbA) return;  // the rounded-up grid's tail (whole workgroup)
+  const wf::Tabs tw = wf::fill_tables<64 * CZB_WC>(lds, a.tw1024, threadIdx.x);
+  const int bc = blkid / a.ncbA, qb = blkid - bc * a.ncbA;
+  const int q = qb * CB + hb * CZB_WC + wave;
+  const bool live = q < a.outH;  // every wave takes part in the block loads and barriers
   const int c = bc % a.C;
   const float lam = a.lam[c];
   const float k = 6.283185307179586f / lam;
   const RsPhase rph = rs_phase(lam, a.z);
-  const float4* vblk = reinterpret_cast<const float4*>(V + ((size_t)bc * a.ncbA + qb) * CB * a.H);
+  const float4* vblk = reinterpret_cast<const float4*>(V + ((size_t)bc * a.ncbA + qb) * CB * a.H) + hb * (CZB_WC / 2);
   const float2* pre = ws + a.preB + (size_t)c * a.tabStride;
   const float2* post = ws + a.postB + (size_t)c * a.tabStride;
   const float2* G = ws + a.ftB + (size_t)c * a.pb.nb * wf::N;
@@ -383,31 +399,34 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
   const float yq = lin(-(float)a.outW * a.ody / 2.0f, (float)a.outW * a.ody / 2.0f, a.outW, q);
   const float xlo = -(float)a.outH * a.odx / 2.0f, xhi = (float)a.outH * a.odx / 2.0f;
   const float cst = ((a.z * a.odx) * a.ody) * lam;
-  const float2* mine = tile + wave * CZB_TP;
   float2 acc[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) acc[i] = make_float2(0.f, 0.f);
   for (int b = 0; b < a.pb.nb; ++b) {
     const int h0 = CZB_BS * b;
-    // the block's [CZB_BS rows][16 columns] run: 4 x 16 B per thread, coalesced
+    // the half block's [CZB_BS rows][8 columns]: 4 x 16 B per thread (row e / 4, columns 2 (e % 4) + {0, 1})
     float4 t4[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = (int)threadIdx.x + 1024 * i;  // float4 index: row e / 8, columns 2 (e % 8) + {0, 1}
-      if (!PARTIAL || h0 + (e >> 3) < m) {
+      const int e = (int)threadIdx.x + 64 * CZB_WC * i;
+      if (!PARTIAL || h0 + (e >> 2) < m) {
         typedef float f32x4 __attribute__((ext_vector_type(4)));
-        const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(vblk) + (size_t)h0 * (CB / 2) + e);
+        const f32x4 t = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(vblk) + (size_t)(h0 + (e >> 2)) * (CB / 2) + (e & 3));
         t4[i] = make_float4(t.x, t.y, t.z, t.w);
       } else {
         t4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
-    __syncthreads();  // the previous block's readers are done with the tile
+    __syncthreads();  // every wave is done with its image (the previous block's transform)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = (int)threadIdx.x + 1024 * i, row = e >> 3, col = 2 * (e & 7);
-      tile[col * CZB_TP + row] = make_float2(t4[i].x, t4[i].y);
-      tile[(col + 1) * CZB_TP + row] = make_float2(t4[i].z, t4[i].w);
+      const int e = (int)threadIdx.x + 64 * CZB_WC * i, row = e >> 2, col = 2 * (e & 3);
+      float* d0 = img0 + col * CZB_IMS + row;
+      float* d1 = d0 + CZB_IMS;
+      d0[0] = t4[i].x;
+      d0[CZB_IMM] = t4[i].y;
+      d1[0] = t4[i].z;
+      d1[CZB_IMM] = t4[i].w;
     }
     __syncthreads();
     if (live) {
@@ -417,7 +436,7 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
       auto mac = [&](int i, float2 x) { acc[i] = cadd(acc[i], cmul(x, Gb[64 * (i >> 2) + 256 * (i & 3)])); };
       auto ldb = [&](int u) {
         if (PARTIAL && h0 + u >= m) return make_float2(0.f, 0.f);
-        return cmul(mine[u], (pre + h0)[u]);
+        return cmul(make_float2(img[u], img[CZB_IMM + u]), (pre + h0)[u]);
       };
       wf::forward<true>(img, tw, ln, ldb, mac);
     }
@@ -767,9 +786,19 @@ static int czt_tables_for(const CztArgs& a, const thz_czt_desc* d, float2* ws, h
   if ((int)g_tabs.size() >= CZT_TAB_MAX || g_tab_bytes + bytes > CZT_TAB_MAX_BYTES)
     return czt_build_tables(a, d, ws, s);
   CztTabEntry en{};
-  THZ_HIP_CHECK(hipMalloc(&en.buf, bytes));
+  // A cache entry needs a hipMalloc and an event; both are refused while another thread has a
+  // stream in a global-mode capture (or when memory is short).  Then this call builds its tables in
+  // its own workspace, as an uncached call does, instead of failing.
+  if (hipEventCreateWithFlags(&en.ready, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    return czt_build_tables(a, d, ws, s);
+  }
+  if (hipMalloc(&en.buf, bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipEventDestroy(en.ready);
+    return czt_build_tables(a, d, ws, s);
+  }
   int e = czt_build_tables(a, d, en.buf, s);
-  if (e == THZ_OK) e = hipEventCreateWithFlags(&en.ready, hipEventDisableTiming) == hipSuccess ? THZ_OK : THZ_E_HIP;
   if (e == THZ_OK) e = hipEventRecord(en.ready, s) == hipSuccess ? THZ_OK : THZ_E_HIP;
   if (e != THZ_OK) {
     // the buffer may still be in use by launched work: keep it (leaked) rather than free it early
@@ -840,7 +869,9 @@ extern "C" int thz_czt_forward(const thz_czt_desc* d, const void* in, void* out,
   {
     KernelTimer kt("czt_cols", s);
     if (a.pb.nb) {
-      hipLaunchKernelGGL(d->H % CZB_BS ? czt_cols_blk<true> : czt_cols_blk<false>, dim3(a.BC * a.ncbA), dim3(64 * CZB_WC), czb_cols_lds_bytes(),
+      // two half-block workgroups per V block; the grid rounded up to whole runs of 16 ids (sibling
+      // halves b and b ^ 8), the ids past the last block exit at once
+      hipLaunchKernelGGL(d->H % CZB_BS ? czt_cols_blk<true> : czt_cols_blk<false>, dim3((a.BC * a.ncbA + 7) / 8 * 16), dim3(64 * CZB_WC), czb_cols_lds_bytes(),
                          s, (const float2*)V, (float2*)out, ws, a);
     } else {
       THZ_CZT_SWITCH(a.pb.np2, czt_cols, dim3(a.BC * d->outH), dim3(threads_pow2_or(a.pb.np2)),

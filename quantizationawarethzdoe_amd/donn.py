@@ -232,20 +232,20 @@ class DONNTrainer:
             self.optimizer.zero_grad(set_to_none=True)
             if not self.allreduce.active or (self.capture_collective and self.allreduce.capturable):
                 # no collective, or a captured one: the whole step is one graph, one replay per step
-                try:
-                    g_fb = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
+                from quantizationawarethzdoe_amd.qat import agreed_capture
+
+                def whole():
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                         loss = self._fb(su, st, frac)
                         self.allreduce.reduce()
                         self._opt()
-                    return g_fb, None, loss
-                except RuntimeError as e:
-                    if not self.allreduce.active:
-                        raise
-                    from quantizationawarethzdoe_amd.qat import _warn_capture
-                    _warn_capture(e)  # same code on every rank: all of them fall back together
-                    self.capture_collective = False
-                    self.optimizer.zero_grad(set_to_none=True)
+                    return g, loss
+                res = agreed_capture(self.allreduce, whole)
+                if res is not None:
+                    return res[0], None, res[1]
+                self.capture_collective = False  # every rank falls back (agreed_capture)
+                self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
                 loss = self._fb(su, st, frac)

@@ -172,6 +172,30 @@ def _warn_capture(e):
                   "falling back to split graphs around an eager all-reduce", RuntimeWarning)
 
 
+def agreed_capture(allreduce, capture_fn):
+    """Capture the whole step with the collective inside it (``capture_fn() -> (graph, loss)``),
+    with every rank agreeing on the outcome: after the attempt, an eager all_reduce(MIN) of a
+    success flag outside any capture.  Returns capture_fn's result, or None when the capture failed
+    on ANY rank -- every rank then discards its graph and builds the split form (fwd/bwd graph, eager
+    all-reduce, optimiser graph), so no rank replays a graph with a captured collective while
+    another runs the eager one.  Without an active collective a capture error is raised as is."""
+    ok, res, err = 1, None, None
+    try:
+        res = capture_fn()
+    except RuntimeError as e:
+        if not allreduce.active:
+            raise
+        ok, err = 0, e
+    if allreduce.active:
+        flag = torch.tensor([ok], dtype=torch.int32, device=allreduce.flat.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=allreduce.group)
+        ok = int(flag.item())
+    if not ok:
+        _warn_capture(err if err is not None else "the capture failed on another rank")
+        return None
+    return res
+
+
 class GradientAllReduce:
     """Average the gradients of ``params`` over the process group with ONE flat all-reduce.
 
@@ -344,19 +368,18 @@ class QATTrainer:
             if not self.allreduce.active or (self.capture_collective and self.allreduce.capturable):
                 # no collective, or a captured one: the whole step (fwd/bwd, all-reduce, Adam) is
                 # one graph, one replay per step
-                try:
-                    g_fb = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
+                def whole():
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
                         loss = self._fb(frac)
                         self.allreduce.reduce()
                         self._opt()
-                    return g_fb, None, loss
-                except RuntimeError as e:
-                    if not self.allreduce.active:
-                        raise
-                    _warn_capture(e)  # same code on every rank: all of them fall back together
-                    self.capture_collective = False
-                    self.optimizer.zero_grad(set_to_none=True)
+                    return g, loss
+                res = agreed_capture(self.allreduce, whole)
+                if res is not None:
+                    return res[0], None, res[1]
+                self.capture_collective = False  # every rank falls back (agreed_capture)
+                self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
                 loss = self._fb(frac)

@@ -44,12 +44,18 @@ def main():
         if os.path.exists(p):
             for k, d in per_kernel(p).items():
                 summ.setdefault(k, {}).update(d)
-    traffic = {}
+    import datetime
+    traffic = {"_meta": {"profile": f"profiles/{tag}_pmc_summary.json", "date": datetime.date.today().isoformat(),
+                         "note": "per-launch HBM bytes of the bench's cfg2 kernels, keyed by bench.py's timer names"}}
+    # kernel name -> the KernelTimer name bench.py reports it under (the four-step column pass is
+    # timed as asm_cols)
+    alias = {"asm_cols_4s": "asm_cols", "asm_cols_pair": "asm_cols"}
     for k, d in summ.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             b = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
             d["hbm_bytes_per_launch"] = b
-            traffic[k.split("<")[0]] = int(b)
+            base = k.split("<")[0]
+            traffic[alias.get(base, base)] = int(b)
     with open(os.path.join(prof, f"{tag}_pmc_summary.json"), "w") as fh:
         json.dump(summ, fh, indent=1)
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as fh:

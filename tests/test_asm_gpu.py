@@ -290,6 +290,49 @@ def test_asm_four_step_k2_matches_three_stage(tmp_path):
     assert rel_l2(res[0], res[1]) <= 2e-6
 
 
+_M3_SCRIPT = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, {root!r})
+from quantizationawarethzdoe_amd.propagation import asm_apply
+g = torch.Generator(device="cuda:0").manual_seed(5)
+x = torch.randn(6, 2, 100, 100, dtype=torch.complex64, device="cuda:0", generator=g)
+lam = [float(torch.tensor(2.998e8 / f, dtype=torch.float32)) for f in (300e9, 250e9)]
+sp = [1e-3, 1e-3]
+one = asm_apply(x, lam, sp, [0.02], 100, 100, True, 1)
+multi = asm_apply(x, lam, sp, [0.02, 0.05, 0.2], 100, 100, True, 1)
+adj = asm_apply(x, lam, sp, [0.02], 100, 100, True, 1, adjoint=True)
+from quantizationawarethzdoe_amd.propagation import asm_propagate_loss
+xr = x.clone().requires_grad_(True)
+tgt = torch.rand(1, 1, 100, 100, device="cuda:0", generator=g)
+o, loss = asm_propagate_loss(xr, tgt, lam, sp, 0.02, 100, 100)
+loss.backward()
+np.save({path!r}, np.concatenate([t.detach().cpu().numpy().reshape(-1).astype(np.complex64)
+                                  for t in (one, multi, adj, o, loss.reshape(1), xr.grad)]))
+"""
+
+
+def test_asm_p300_three_by_100_column_pass_matches_5345(tmp_path):
+    """The P = 300 column pass as three 100-point transforms per column (asm_cols_m3: two columns per
+    wave, radix 10 x 10; the one-z kernel and the Z-loop kernel), with the row passes on the same
+    split (asm_rows_fwd_m3, asm_rows_inv_m3 and its fused-loss form), against the 5 3 4 5
+    mixed-radix kernels (THZ_K2_M3=0) on the layers' geometry (100^2 fields, padding 2, cropped):
+    batch 6, two wavelengths, one z, three z, the adjoint, and the fused ASM -> loss with its
+    gradient.  Same transforms, other rounding order: rel-L2 <= 2e-6."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for flag in ("1", "0"):
+        path = str(tmp_path / f"m3_{flag}.npy")
+        env = dict(os.environ, THZ_K2_M3=flag)
+        r = subprocess.run([sys.executable, "-c", _M3_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(np.load(path))
+    assert rel_l2(res[0], res[1]) <= 2e-6
+
+
 def test_asm_p2048_64_planes_every_plane_vs_oracle():
     """asm_cols<2048> over 64 planes in two full 32-plane chunks (the kparts split of each chunk's
     last dispatch round included): every plane vs the fp64 oracle, <= max(1e-4, 1.5 x the oracle's

@@ -57,6 +57,45 @@ def test_gradient_allreduce_gloo_world2():
     assert all(ok and has for _, ok, has in res), res
 
 
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+        from quantizationawarethzdoe_amd.qat import GradientAllReduce, agreed_capture
+        ar = GradientAllReduce([torch.nn.Parameter(torch.zeros(4))])
+
+        def fails_on_rank1():
+            if rank == 1:
+                raise RuntimeError("capture refused on this rank")
+            return "graph", 1.0
+
+        with warnings.catch_warnings(record=True):
+            warnings.simplefilter("always")
+            mixed = agreed_capture(ar, fails_on_rank1)
+            both = agreed_capture(ar, lambda: ("graph", 2.0))
+        q.put((rank, mixed, both))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_agreed_capture_falls_back_on_every_rank_gloo_world2():
+    """a capture failure on ONE rank makes every rank take the split form (the
+    eager MIN of a success flag after the attempt); a capture that succeeds everywhere is kept."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r[1] for r in res] == [None, None]
+    assert [r[2] for r in res] == [("graph", 2.0), ("graph", 2.0)]
+
+
 def test_donn_detector_targets_and_cpu_refusal():
     """cfg5: ten disjoint det x det detector targets; the trainer refuses a CPU model loudly."""
     from quantizationawarethzdoe_amd import donn

@@ -150,3 +150,18 @@ def test_asm_forward_refuses_multi_valued_z():
     prop.z = [0.3, 0.4, 0.5]
     with pytest.raises(ValueError, match="propagate_planes"):
         prop(f)
+
+
+def test_czt_one_by_one_power_of_two_width_output_stays_in_the_graph():
+    """ADVICE round 3: the reference's [B, C, 1, 0] CZT output (1 x 1 output, power-of-two W, odd H;
+    Props/CZT_Prop.py:206,211) is an empty tensor that stays in the autograd graph; backward through
+    it gives the input a zero gradient instead of raising 'does not require grad'.  No kernel runs."""
+    import torch
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.CZT_Prop import CZT_prop
+    x = torch.randn(1, 1, 3, 4, dtype=torch.complex64, requires_grad=True)
+    f = ElectricField(data=x, wavelengths=1e-3, spacing=1e-3, device="cpu")
+    out = CZT_prop(z_distance=0.1, device="cpu")(f, outputHeight=1, outputWidth=1)
+    assert tuple(out.data.shape) == (1, 1, 1, 0)
+    out.data.abs().sum().backward()
+    assert x.grad is not None and float(x.grad.abs().sum()) == 0.0
