@@ -182,8 +182,14 @@ class DONNTrainer:
         loss = self._loss(u, target, frac)
         # preallocated d loss / d loss: no fill kernel per step
         loss.backward(gradient=self._one if loss.dtype == self._one.dtype and loss.device == self._one.device else None)
+        from quantizationawarethzdoe_amd.qat import release_step_graph
+        release_step_graph([self.model])
         self.allreduce.pack()
-        return loss
+        # detached: the returned (graph-static) loss must not hold the step's autograd graph, whose
+        # AccumulateGrad nodes -- made on the warm-up stream -- would otherwise outlive the capture and
+        # be reused by the next capture's backward on another stream (torch's "AccumulateGrad node's
+        # stream does not match" warning)
+        return loss.detach()
 
     def _opt(self):
         self.allreduce.unpack()

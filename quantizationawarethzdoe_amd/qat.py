@@ -172,6 +172,20 @@ def _warn_capture(e):
                   "falling back to split graphs around an eager all-reduce", RuntimeWarning)
 
 
+def release_step_graph(modules):
+    """After a step's backward: the DOE layers keep their last quantized ``height_map`` (the
+    reference's attribute, read by visualize() / save()) detached.  Attached, it holds the step's
+    autograd graph -- down to the weight's AccumulateGrad node -- alive until the next forward, so
+    a HIP-graph capture would reuse the node its warm-up made on another stream (torch's
+    "AccumulateGrad node's stream does not match" warning).  The values are
+    unchanged (a detached view of the same storage, which graph replays keep updating)."""
+    for m in modules:
+        for layer in m.modules():
+            h = layer.__dict__.get("height_map")
+            if torch.is_tensor(h) and not isinstance(h, nn.Parameter) and h.grad_fn is not None:
+                layer.height_map = h.detach()
+
+
 def agreed_capture(allreduce, capture_fn):
     """Capture the whole step with the collective inside it (``capture_fn() -> (graph, loss)``),
     with every rank agreeing on the outcome: after the attempt, an eager all_reduce(MIN) of a
@@ -318,8 +332,13 @@ class QATTrainer:
             loss = self.loss_fn(out.data, self.target)
         # d loss / d loss = 1 from a preallocated tensor: no fill kernel per step
         loss.backward(gradient=self._one if loss.dtype == self._one.dtype and loss.device == self._one.device else None)
+        release_step_graph([self.system])
         self.allreduce.pack()
-        return loss
+        # detached: the returned (graph-static) loss must not hold the step's autograd graph, whose
+        # AccumulateGrad nodes -- made on the warm-up stream -- would otherwise outlive the capture and
+        # be reused by the next capture's backward on another stream (torch's "AccumulateGrad node's
+        # stream does not match" warning)
+        return loss.detach()
 
     def _opt(self):
         self.allreduce.unpack()

@@ -83,3 +83,38 @@ def test_donn_captured_allreduce_matches_split_graphs(one_rank_rccl):
     assert all(torch.equal(a, b) for a, b in zip(res[False][1], res[True][1]))
     print(f"\ncfg5 DONN step (batch 32), one-rank RCCL all-reduce: split {res[False][2]:.4f} ms, "
           f"captured {res[True][2]:.4f} ms")
+
+
+@pytest.mark.parametrize("which", ["qat", "donn"])
+def test_captured_trainers_keep_no_autograd_graph_alive(which):
+    """the captured trainers used to keep a step's autograd graph alive (the DOE
+    layer's attached ``height_map`` and the returned loss), so the next capture's backward reused
+    the weight's AccumulateGrad node made on the warm-up stream and torch warned "AccumulateGrad
+    node's stream does not match".  Three schedule phases (three captures) run warning-free, the
+    layer's height map carries no grad_fn after a step, and the returned loss is detached."""
+    import warnings
+    from quantizationawarethzdoe_amd import donn, qat
+    dev = torch.device("cuda:0")
+    torch.manual_seed(7)
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        if which == "qat":
+            system = qat.FourFocalSpotsSystem(device=dev)
+            tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=100, graph=True)
+            for frac in (0.1, 0.1, 0.5, 0.5, 0.9, 0.9):
+                loss = tr.step(frac)
+            layers = [system.doe]
+        else:
+            model = donn.DONN(device=dev, q_method="sgs")
+            tr = donn.DONNTrainer(model, donn.detector_targets(device=dev), graph=True)
+            u = torch.rand(4, 1, 100, 100, device=dev)
+            lab = torch.randint(0, 10, (4,), device=dev)
+            for frac in (0.1, 0.1, 0.5, 0.5, 0.9, 0.9):
+                loss = tr.step(u, lab, frac)
+            layers = list(model.does)
+        torch.cuda.synchronize()
+    bad = [str(w.message) for w in rec if "AccumulateGrad" in str(w.message)]
+    assert not bad, bad[:2]
+    assert loss.grad_fn is None and torch.isfinite(loss)
+    for d in layers:
+        assert getattr(d, "height_map").grad_fn is None
