@@ -626,8 +626,10 @@ __global__ void __launch_bounds__(1024) asm_cols_zsum(const float2* __restrict__
 // the cfg2 parity tests.  Props/ASM_Prop.py:314-378 (the per-z ift2 over the padded column).
 namespace fs {
 constexpr int N = 8192, T = 512;
-constexpr int SL = 64 * 17;  // float2 per wave slice: the exchange image (g, c) x e padded to 17
-constexpr int IMG = 8706;    // >= lds_floats2(8192) (the forward transform's image) and 8 SL
+// float2 per wave slice: the exchange image (g, c) x e padded to 17 (1088), +4 so that the eight
+// slices' same positions fall on distinct banks (K3's output transpose reads all eight in one access)
+constexpr int SL = 64 * 17 + 4;
+constexpr int IMG = 8 * SL;  // >= lds_floats2(8192) (the forward transform's image)
 constexpr int TINV = 15 * 64;  // w1024^(lane c), [c - 1][lane]
 constexpr int T64 = 3 * 16;    // w64^(g e), [g - 1][e]
 constexpr int TW8 = 64 + 16;   // w8192^n2 = w8192^(n2 & 63) w128^(n2 >> 6), n2 < 1024
@@ -641,6 +643,57 @@ __device__ __forceinline__ void swap_rows16(float& a, float& b) {
   const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(b), false, false);
   a = __int_as_float(r[0]);
   b = __int_as_float(r[1]);
+}
+
+// The 1024-point inverse transform of one wave (the four-step K2 / K3): on entry x[j] holds input
+// k2 = lane + 64 j, on exit x[h] holds output lane + 64 h.  Radix 16 over j in registers, twiddle
+// w1024^(lane c); the 64-point transform over the lane index a = e + 16 f: v_permlane32/16_swap
+// trade lane bits 5, 4 (f) for register bits 0, 1 (c0, c1), radix 4 over f, twiddle w64^(g e),
+// one exchange through this wave's own LDS slice (no workgroup barrier), radix 16 over e.
+// `before` runs just before the slice's first write (the caller's barrier, if other waves may
+// still read the slice).
+template <class Before>
+__device__ __forceinline__ void wave_ifft1024(float2 (&x)[16], int lane, float2* slice, const float2* tinv,
+                                              const float2* t64, Before before) {
+  dft16<true>(x);
+#pragma unroll
+  for (int q = 1; q < 16; ++q) x[q] = cmulc(x[q], tinv[(q - 1) * 64 + lane]);
+  // lane bit 5 <-> register bit 0, lane bit 4 <-> register bit 1: lane e + 16 c1 + 32 c0,
+  // register f1 + 2 f0 + 4 u (u = c >> 2)
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    swap_halves(x[2 * p].x, x[2 * p + 1].x);
+    swap_halves(x[2 * p].y, x[2 * p + 1].y);
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    if (q & 2) continue;
+    swap_rows16(x[q].x, x[q + 2].x);
+    swap_rows16(x[q].y, x[q + 2].y);
+  }
+  // radix 4 over f = f0 + 2 f1 (registers 4u + {0, 2, 1, 3}); output g at 4u + {0, 2, 1, 3}
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    float2* v = &x[4 * u];
+    dft4<true>(v[0], v[2], v[1], v[3]);
+    v[2] = cmulc(v[2], t64[lane & 15]);
+    v[1] = cmulc(v[1], t64[16 + (lane & 15)]);
+    v[3] = cmulc(v[3], t64[32 + (lane & 15)]);
+  }
+  before();
+  // exchange image positions: write (g, c, e) at (16 g + c) 17 + e from lane e + 16 c1 + 32 c0,
+  // read e at 17 lane + e
+  const int xw = ((lane >> 5) + 2 * ((lane >> 4) & 1)) * 17 + (lane & 15);
+  const int xr = 17 * lane;
+#pragma unroll
+  for (int rho = 0; rho < 16; ++rho) {
+    const int u = rho >> 2, g = ((rho & 1) << 1) | ((rho >> 1) & 1);
+    slice[xw + (16 * g + 4 * u) * 17] = x[rho];
+  }
+  wf::wave_sync();
+#pragma unroll
+  for (int e = 0; e < 16; ++e) x[e] = slice[xr + e];
+  dft16<true>(x);  // x[h] = output lane + 64 h
 }
 
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
@@ -741,50 +794,10 @@ asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, As
       sincos_hw(tf_mul(z, sq[j]), &sn, &cs);
       x[j] = cmul(sp[j], make_float2(cs, a.adjoint ? -sn : sn));
     }
-    // step 1: radix 16 over j, then w1024^(+lane c)
-    dft16<true>(x);
-#pragma unroll
-    for (int q = 1; q < 16; ++q) x[q] = cmulc(x[q], tinv[(q - 1) * 64 + lane]);
-    // lane bit 5 <-> register bit 0, lane bit 4 <-> register bit 1: lane e + 16 c1 + 32 c0,
-    // register f1 + 2 f0 + 4 u (u = c >> 2)
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      swap_halves(x[2 * p].x, x[2 * p + 1].x);
-      swap_halves(x[2 * p].y, x[2 * p + 1].y);
-    }
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      if (q & 2) continue;
-      swap_rows16(x[q].x, x[q + 2].x);
-      swap_rows16(x[q].y, x[q + 2].y);
-    }
-    // radix 4 over f = f0 + 2 f1 (registers 4u + {0, 2, 1, 3}); output g at 4u + {0, 2, 1, 3}
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float2* v = &x[4 * u];
-      dft4<true>(v[0], v[2], v[1], v[3]);
-      v[2] = cmulc(v[2], t64[lane & 15]);
-      v[1] = cmulc(v[1], t64[16 + (lane & 15)]);
-      v[3] = cmulc(v[3], t64[32 + (lane & 15)]);
-    }
-    __syncthreads();  // A: the previous z's radix-8 reads of every slice are done
-    float2* const slice = lds + w * fs::SL;
-    // exchange image positions: write (g, c, e) at (16 g + c) 17 + e from lane e + 16 c1 + 32 c0,
-    // read e at 17 lane + e
-    const int xw = ((lane >> 5) + 2 * ((lane >> 4) & 1)) * 17 + (lane & 15);
-    const int xr = 17 * lane;
-#pragma unroll
-    for (int rho = 0; rho < 16; ++rho) {
-      const int u = rho >> 2, g = ((rho & 1) << 1) | ((rho >> 1) & 1);
-      slice[xw + (16 * g + 4 * u) * 17] = x[rho];
-    }
+    wave_ifft1024(x, lane, lds + w * fs::SL, tinv, t64, [] { __syncthreads(); });  // A: the previous z's radix-8 reads are done
     wf::wave_sync();
 #pragma unroll
-    for (int e = 0; e < 16; ++e) x[e] = slice[xr + e];
-    dft16<true>(x);  // x[h] = Z_k1[lane + 64 h]
-    wf::wave_sync();
-#pragma unroll
-    for (int h = 0; h < 16; ++h) slice[lane + 64 * h] = x[h];
+    for (int h = 0; h < 16; ++h) lds[w * fs::SL + lane + 64 * h] = x[h];
     __syncthreads();  // B: every Z_k1 is in its slice
     float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
 #pragma unroll
@@ -812,6 +825,90 @@ asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, As
         // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2)
         if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v[n1];
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// K3 at Pw = 8192 as a four-step transform (opt-in THZ_K3_4S=1, A/B against asm_rows_inv<8192>).
+// With k = 1024 k1 + k2 and n = n1 + 8 n2 the inverse is
+//   y[n1 + 8 n2] = sum_k2 w1024^(n2 k2) [ w8192^(n1 k2) sum_k1 w8^(n1 k1) X[1024 k1 + k2] ],
+// so each thread gathers its two k2 (the band columns of consecutive lanes are consecutive, as in
+// asm_rows_inv) for all k1, runs the radix 8 over k1 in registers, and after ONE workgroup exchange
+// wave n1 runs the 1024-point wave transform over k2 (wave_ifft1024, no workgroup barrier).  A
+// second exchange gives each thread consecutive outputs n for whole-line streaming stores.  Three
+// barriers per row instead of the split-exchange transform's twelve; RPW rows per workgroup share
+// one fill of the twiddle tables.
+constexpr int K3_RPW = 4;
+constexpr size_t k3_4s_lds_bytes() { return (size_t)(fs::IMG + fs::TINV + fs::T64 + fs::TW8) * sizeof(float2); }
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+asm_rows_inv_4s(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw, AsmArgs a) {
+  constexpr int PN = fs::N, TT = fs::T;
+  extern __shared__ float2 lds[];
+  float2* const tinv = lds + fs::IMG;
+  float2* const t64 = tinv + fs::TINV;
+  float2* const tw8 = t64 + fs::T64;
+  const float2* __restrict__ tw = pw.tw;  // exp(-2 pi i t / 8192)
+  const int tid = threadIdx.x, w = tid >> 6;
+  for (int i = tid; i < fs::TINV; i += TT) tinv[i] = tw[8 * (i & 63) * ((i >> 6) + 1)];
+  if (tid < fs::T64) t64[tid] = tw[128 * ((tid >> 4) + 1) * (tid & 15)];
+  if (tid < fs::TW8) tw8[tid] = tw[tid < 64 ? tid : 64 * (tid - 64)];
+  const int rows = a.nz * a.BC * a.Hout;
+  for (int rr = 0; rr < K3_RPW; ++rr) {
+    const int row = (int)blockIdx.x * K3_RPW + rr;
+    if (row >= rows) break;  // uniform over the workgroup
+    const int plane = row / a.Hout, ro = row - plane * a.Hout;
+    const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    // gather X[1024 k1 + k2] of this thread's k2 = tid + 512 s, then radix 8 over k1 and the
+    // four-step twiddle w8192^(n1 k2)
+    float2 v[2][8];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k2 = tid + 512 * s;
+#pragma unroll
+      for (int k1 = 0; k1 < 8; ++k1) {
+        const int c = band_col(1024 * k1 + k2, PN, a.J, a.ncols);
+        v[s][k1] = c >= 0 ? src[blk_u(c, ro, a.Hout)] : make_float2(0.f, 0.f);
+      }
+    }
+    if (rr == 0) __syncthreads();  // the tables (their first reads follow)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int k2 = tid + 512 * s;
+      dft8<true>(v[s]);
+      const float2 w1 = cmul(tw8[k2 & 63], tw8[64 + (k2 >> 6)]);
+      const float2 w2 = cmul(w1, w1), w3 = cmul(w1, w2), w4 = cmul(w2, w2);
+      v[s][1] = cmulc(v[s][1], w1);
+      v[s][2] = cmulc(v[s][2], w2);
+      v[s][3] = cmulc(v[s][3], w3);
+      v[s][4] = cmulc(v[s][4], w4);
+      v[s][5] = cmulc(v[s][5], cmul(w1, w4));
+      v[s][6] = cmulc(v[s][6], cmul(w2, w4));
+      v[s][7] = cmulc(v[s][7], cmul(w3, w4));
+    }
+    __syncthreads();  // the previous row's output reads of every slice are done
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int n1 = 0; n1 < 8; ++n1) lds[n1 * fs::SL + tid + 512 * s] = v[s][n1];
+    __syncthreads();
+    float2* const slice = lds + w * fs::SL;  // wave n1 = w
+    float2 x[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) x[j] = slice[lane + 64 * j];
+    wave_ifft1024(x, lane, slice, tinv, t64, [] {});  // only this wave reads its slice now
+    wf::wave_sync();
+#pragma unroll
+    for (int h = 0; h < 16; ++h) slice[lane + 64 * h] = x[h];  // y[w + 8 (lane + 64 h)]
+    __syncthreads();
+    float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + ro) * a.Wout;
+    for (int wo = tid; wo < a.Wout; wo += TT) {
+      const int n = a.out_c0 + wo;
+      // written once and never read back here: streaming stores (asm_rows_inv)
+      st_stream(dst + wo, lds[(n & 7) * fs::SL + (n >> 3)]);
     }
   }
 }
@@ -1655,6 +1752,9 @@ static int ensure_lds_attr() {
     const hipError_t e4 = hipFuncSetAttribute((const void*)asm_cols_4s, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)fs::lds_bytes(THZ_MAX_Z));
     if (e4 != hipSuccess) err = e4;
+    const hipError_t e5 = hipFuncSetAttribute((const void*)asm_rows_inv_4s,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3_4s_lds_bytes());
+    if (e5 != hipSuccess) err = e5;
   });
   if (err != hipSuccess) return fail(THZ_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s",
                                      hipGetErrorString(err));
@@ -1693,6 +1793,15 @@ static bool k2_4s(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == fs::N && !a.tft && !a.zsum;
 }
+// Four-step K3 (asm_rows_inv_4s) at Pw = 8192, opt-in THZ_K3_4S=1 (A/B against asm_rows_inv<8192>).
+static bool k3_4s(int Pw) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K3_4S");
+    return e && e[0] == '1';
+  }();
+  return on && Pw == fs::N;
+}
+
 // The 3 x 100 row passes (asm_rows_fwd_m3 / asm_rows_inv_m3) at Pw = 300 with the input (K1) or
 // output (K3) columns [100, 200); THZ_K2_M3=0 selects the 5 3 4 5 row kernels too.
 static bool m3_on() {
@@ -1918,6 +2027,9 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
       } else if (m3) {
         hipLaunchKernelGGL(asm_rows_inv_m3<false>, g3, dim3(64), m3_lds_bytes(), s, (const float2*)U, (float2*)out, pw,
                            a);
+      } else if (k3_4s(g.Pw)) {
+        hipLaunchKernelGGL(asm_rows_inv_4s, dim3((a.nz * g.BC * g.Hout + K3_RPW - 1) / K3_RPW), dim3(fs::T),
+                           k3_4s_lds_bytes(), s, (const float2*)U, (float2*)out, pw, a);
       } else {
         THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
                         (float2*)out, pw, a);

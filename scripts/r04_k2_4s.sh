@@ -13,5 +13,7 @@ THZ_K2_4S=1 bash $S 200 $o/bench_4s_a.log python $B &&
 THZ_K2_4S=0 bash $S 200 $o/bench_3s_a.log python $B &&
 THZ_K2_4S=1 bash $S 200 $o/bench_4s_b.log python $B &&
 THZ_K2_4S=0 bash $S 200 $o/bench_3s_b.log python $B &&
+THZ_K3_4S=1 bash $S 200 $o/bench_k3_4s_a.log python $B &&
+THZ_K3_4S=1 bash $S 200 $o/bench_k3_4s_b.log python $B &&
 bash $S 400 $o/bench_full.log python bench.py --no-cpu-baseline &&
 bash $S 400 $o/qat_quality.log python -u scripts/qat_quality.py --seeds 5 --out $o/qat_quality.json

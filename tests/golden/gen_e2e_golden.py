@@ -79,7 +79,10 @@ def fom(ref, resolution, dxy, lam, focal, pos, dt):
     return ref.HF.normalize(psf.unsqueeze(0).unsqueeze(0))
 
 
-def run(ref, hmap, f64):
+def run(ref, hmap, f64, force_max=None):
+    """The system's field, loss and height gradient; ``force_max`` = (i, j) divides by the intensity
+    of that pixel instead of normalize()'s max (the same value when the pixel is a maximum, and
+    the gradient torch's max routes to that index)."""
     GB = ref.import_module("LightSource.Gaussian_beam")
     TL = ref.import_module("Components.Thin_Lens")
     AP = ref.import_module("Components.Aperture")
@@ -107,7 +110,11 @@ def run(ref, hmap, f64):
                                     bandlimit_kernel=True, device="cpu")
             out = asm3(doe(field_in))
         target = sum(fom(ref, [100, 100], 1 * MM, lam, 200 * MM, [a * MM, b * MM], dt) for a, b in FOCI9)
-        amp = ref.HF.normalize(torch.abs(out.data) ** 2)
+        inten = torch.abs(out.data) ** 2
+        if force_max is None:
+            amp = ref.HF.normalize(inten)
+        else:
+            amp = inten / inten[0, 0, force_max[0], force_max[1]]
         loss = torch.nn.MSELoss()(amp, target)
         loss.backward()
         return dict(field_in=field_in.data.detach().numpy(), out=out.data.detach().numpy(), loss=float(loss.detach()),
@@ -147,11 +154,21 @@ def main():
                 arrays[f"field_in{tag}"] = r["field_in"]
                 arrays[f"target{tag}"] = r["target"]
             print(f"{name} fp{tag}: loss {r['loss']:.9e}", flush=True)
+        # tied maxima (the trained maps are mirror-symmetric): normalize()'s max is a tie-break of
+        # rounding, and its gradient term moves with it -- store the fp64 gradient for every pixel
+        # within 1e-9 of the maximum, so the GPU test can grade the one its own max picked
+        I64 = np.abs(arrays[f"{name}__out64"][0, 0]) ** 2
+        tied = np.argwhere(I64 >= I64.max() * (1 - 1e-9))
+        ties = []
+        if len(tied) > 1:
+            for i, j in tied:
+                arrays[f"{name}__gradtie_{i}_{j}"] = run(ref, h, True, force_max=(int(i), int(j)))["grad"]
+                ties.append([int(i), int(j)])
         o32, o64 = arrays[f"{name}__out32"], arrays[f"{name}__out64"]
         rel = float(np.linalg.norm(o32 - o64) / np.linalg.norm(o64))
         lv = sorted(set(np.round(h.ravel() * 1e6).tolist()))
         meta.append(dict(name=name, shape=list(h.shape), levels=lv if len(lv) <= 8 else f"{len(lv)} distinct",
-                         rel32vs64=rel, source=sources.get(name, "designed here"),
+                         rel32vs64=rel, source=sources.get(name, "designed here"), tied_max=ties,
                          loss64=float(arrays[f"{name}__loss64"])))
         print(f"  {name}: reference fp32 vs fp64 field rel-L2 {rel:.2e}")
     np.savez_compressed(os.path.join(HERE, "e2e_golden.npz"), **arrays)

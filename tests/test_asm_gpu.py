@@ -269,6 +269,26 @@ np.save({path!r}, np.concatenate([out[:, 0, 0, ::4, ::4].cpu().numpy().reshape(-
 """
 
 
+def test_asm_four_step_k3_matches_split_exchange(tmp_path):
+    """The opt-in four-step row pass (THZ_K3_4S=1, asm_rows_inv_4s: radix 8 over k1 in registers, one
+    workgroup exchange, eight 1024-point wave transforms, a transposing exchange for whole-line
+    stores, four rows per workgroup) against asm_rows_inv<8192> on the cfg2 geometry (the same
+    7 planes and adjoint plane as the K2 comparison).  rel-L2 <= 2e-6."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for flag in ("1", "0"):
+        path = str(tmp_path / f"k3_{flag}.npy")
+        env = dict(os.environ, THZ_K3_4S=flag)
+        r = subprocess.run([sys.executable, "-c", _K2_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(np.load(path))
+    assert rel_l2(res[0], res[1]) <= 2e-6
+
+
 def test_asm_four_step_k2_matches_three_stage(tmp_path):
     """The four-step column pass (asm_cols_4s, the default at Ph = 8192: eight 1024-point wavefront
     transforms and one radix-8 step across the waves per z) against the three-stage asm_cols<8192>
@@ -300,7 +320,7 @@ lam = [float(torch.tensor(2.998e8 / f, dtype=torch.float32)) for f in (300e9, 25
 sp = [1e-3, 1e-3]
 one = asm_apply(x, lam, sp, [0.02], 100, 100, True, 1)
 multi = asm_apply(x, lam, sp, [0.02, 0.05, 0.2], 100, 100, True, 1)
-adj = asm_apply(x, lam, sp, [0.02], 100, 100, True, 1, adjoint=True)
+adj = asm_apply(one, lam, sp, [0.02], 100, 100, True, 1, adjoint=True)
 from quantizationawarethzdoe_amd.propagation import asm_propagate_loss
 xr = x.clone().requires_grad_(True)
 tgt = torch.rand(1, 1, 100, 100, device="cuda:0", generator=g)

@@ -15,7 +15,9 @@ generator (an 80 x 80 map upsampled to the 100 x 100 field, and a 100 x 100 one)
 
 Tolerances: the field before the DOE and the detector field rel-L2 <= 1e-4 (SURVEY §8(c) ASM
 bound; the reference's own fp32 error here is 5e-5), the loss within 1e-4 relative, the height-map
-gradient (d loss / d h through the modulation and the ASM adjoint) within 1e-3 rel-L2.
+gradient (d loss / d h through the modulation and the ASM adjoint) within 1e-3 rel-L2 of the
+reference's fp64 gradient -- for the trained maps, whose symmetric outputs tie the normalize()
+maximum, the gradient for the tied pixel this run's maximum picked (see the test).
 """
 import json
 import os
@@ -74,5 +76,16 @@ def test_designed_doe_through_four_focal_spots_system(case):
     ref_loss = float(A[f"{k}__loss64"])
     assert abs(float(loss.detach()) - ref_loss) <= 1e-4 * ref_loss, (float(loss.detach()), ref_loss)
     g = doe.height_map.grad.detach().cpu().numpy()
-    e_g = rel_l2(g, A[f"{k}__grad64"])
+    ref_g = A[f"{k}__grad64"]
+    if case.get("tied_max"):
+        # The reference's trained maps are mirror-symmetric (num_unit = 2): |E|^2 has four maxima
+        # equal to 1e-15, so normalize()'s max -- and the gradient term it routes to that pixel --
+        # is a tie-break of rounding (the reference's own fp32 and fp64 runs may differ by 100 %).
+        # The fixture holds the fp64 gradient for each tied pixel; grade the one this run's max
+        # picked (torch.max: the first index of the maximum, as normalize() takes it).
+        inten = (torch.abs(out.data.detach()) ** 2).reshape(-1)
+        i, j = divmod(int(torch.argmax(inten)), inten.numel() // 100)
+        assert [i, j] in case["tied_max"], (i, j, case["tied_max"])
+        ref_g = A[f"{k}__gradtie_{i}_{j}"]
+    e_g = rel_l2(g, ref_g)
     assert e_g <= 1e-3, e_g
