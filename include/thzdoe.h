@@ -56,7 +56,7 @@ typedef void* thz_stream_t; /* hipStream_t */
  * struct from an older header would make the library read past it.  Descriptors are plain C
  * structs: zero-initialise them (memset / `= {0}` / ctypes defaults) so fields a caller does not
  * know about stay 0 (no noise buffer and no device generator means no noise). */
-#define THZ_ABI_VERSION 4
+#define THZ_ABI_VERSION 5
 
 /* Library identity. */
 const char* thz_version(void);
@@ -87,6 +87,13 @@ typedef struct thz_asm_desc {
   float dx, dy;
   const float* wavelengths; /* host [C] */
   const float* z;           /* host [Z] */
+  /* optional (NULL = none, ABI 5): an aperture on the output grid (ApertureElement after ASM_prop,
+   * Components/Aperture.py:104-136, e.g. the DONN's layers, experiment_DONN_3_layers.ipynb:109-200),
+   * applied in the row-inverse pass's stores (forward) or in the row pass's loads of the adjoint's
+   * input (the adjoint of mask * ASM is ASM^H * mask).  Its BC is ignored; H, W must be the
+   * output grid's (unpad ? H, W : the padded plane); the field is multiplied by 1 / 0, so NaN / inf
+   * propagate as in the reference's field * mask. */
+  const struct thz_aperture_desc* window_mask;
 } thz_asm_desc;
 
 /* Workspace: the row-pass spectrum T [BC][ncols][H], one z-chunk of column-pass output

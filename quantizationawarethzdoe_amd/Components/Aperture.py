@@ -85,13 +85,35 @@ class ApertureElement(nn.Module):
     def aperture(self, mask):
         self.__dict__["_aperture_set"] = mask
 
+    def _note_input(self, field, shape=None, dtype=None):
+        """The ``.aperture`` attribute's source: the last input's geometry (not its data)."""
+        shape = tuple(field.shape) if shape is None else tuple(shape)
+        self.__dict__.pop("_aperture_set", None)
+        self.__dict__["_aperture_src"] = (self.aperture_type, types.SimpleNamespace(
+            spacing_host=field.spacing_host, height=shape[-2], width=shape[-1], shape=shape,
+            dtype=field.data.dtype if dtype is None else dtype, device=field.device))
+
+    def window_desc(self, field, H, W):
+        """The mask of this aperture on an H x W grid with ``field``'s spacing as a thz_aperture_desc
+        (for thz_asm_desc.window_mask: the aperture folded into the propagation before it), or None
+        for aperture_type None.  The same sizes, clipping and errors as forward()."""
+        dx, dy = field.spacing_host
+        if self.aperture_type == 'rect':
+            return _lib.ApertureDesc(BC=1, H=H, W=W, kind=_lib.APERTURE_RECT, dx=dx, dy=dy,
+                                     half_w=self._rect_half(self.aperture_size, dx, W),
+                                     half_h=self._rect_half(self.aperture_size, dy, H), radius=0.0)
+        if self.aperture_type == 'circ':
+            geo = types.SimpleNamespace(spacing_host=field.spacing_host, height=H, width=W)
+            return _lib.ApertureDesc(BC=1, H=H, W=W, kind=_lib.APERTURE_CIRC, dx=dx, dy=dy, half_w=0.0, half_h=0.0,
+                                     radius=self._circ_radius(geo, self.aperture_size))
+        if self.aperture_type is None:
+            return None
+        raise ValueError('No exisiting aperture shape, please define by yourself')
+
     def forward(self, field: ElectricField) -> ElectricField:
         dx, dy = field.spacing_host
         H, W = field.height, field.width
-        self.__dict__.pop("_aperture_set", None)
-        self.__dict__["_aperture_src"] = (self.aperture_type, types.SimpleNamespace(
-            spacing_host=field.spacing_host, height=H, width=W, shape=tuple(field.shape), dtype=field.data.dtype,
-            device=field.device))
+        self._note_input(field)
         if self.aperture_type == 'rect':
             out = _optics.aperture(field.data, _lib.APERTURE_RECT, dx, dy,
                                    half_w=self._rect_half(self.aperture_size, dx, W),

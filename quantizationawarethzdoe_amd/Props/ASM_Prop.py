@@ -210,8 +210,9 @@ class ASM_prop(nn.Module):
             print("The critical distance is {} m, the TF will be fine during the sampling !".format(zc))
         self.check_Zc = False
 
-    def _run(self, field: ElectricField, zs, loss_target=None):
-        """[Z, B, C, Ho, Wo]; with ``loss_target`` (one z): (out, QAT loss) from the fused pipeline."""
+    def _run(self, field: ElectricField, zs, loss_target=None, out_mask=None):
+        """[Z, B, C, Ho, Wo]; with ``loss_target`` (one z): (out, QAT loss) from the fused pipeline;
+        ``out_mask``: an aperture folded onto the output (propagation.window_mask_fusable geometry)."""
         pend = field._take_pending()
         data = pend.field if pend is not None else field.data
         B, C, H, W = data.shape
@@ -234,10 +235,11 @@ class ASM_prop(nn.Module):
                 out = _prop.asm_propagate_loss(x, loss_target, wl, sp, zs[0], ph, pw, unpad=unpad, bandlimit=bl,
                                                pend=pend if fuse else None)
             elif pend is not None and pend.out is None:  # the DOE layer's modulation, fused into the row pass
-                out = _prop.asm_propagate_modulated(pend, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl)
+                out = _prop.asm_propagate_modulated(pend, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl,
+                                                    mask=out_mask)
             else:
                 x = pend.run() if pend is not None else x
-                out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl)
+                out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl, mask=out_mask)
         except RuntimeError as err:
             print("##################################################")
             print("An error occurred.  If the error was due to insufficient memory, try decreasing the size of the "

@@ -86,6 +86,10 @@ struct AsmArgs {
   float lg_two_inv_n;
   // mixed-radix K2 tables of the first z-chunk computed by tab_blocks extra K1 workgroups
   int tab_blocks;
+  // thz_asm_desc.window_mask: 1 = multiply the K3 stores by the mask (forward), 2 = the K1 loads
+  // (adjoint input); apm is the mask on that grid
+  int ap_side;
+  ApertureArgs apm;
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
@@ -201,6 +205,9 @@ __device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq);
 // The K1 input element s of row h of plane `plane` (s < Win): the field, or what the fused
 // loaders make of it -- the loss gradient of the adjoint of the fused loss, the DOE modulation
 // t_c(h + noise) (writing the noisy height map once), or the VRS Ez plane.
+// AP: apply the window mask of the adjoint's input (only the 300-point row pass carries it: the
+// runtime test costs the 64-VGPR power-of-two row kernels registers)
+template <bool AP>
 struct RowSrc {
   const AsmArgs& a;
   const float2* in;
@@ -240,6 +247,12 @@ struct RowSrc {
     }
   }
   __device__ __forceinline__ float2 operator()(int s) const {
+    const float2 v = value(s);
+    // the adjoint of (window mask) * ASM: the mask on the adjoint's input (NaN / inf propagate)
+    if constexpr (AP) return a.ap_side == 2 && !aperture_open(a.apm, h, s) ? cscale(v, 0.f) : v;
+    else return v;
+  }
+  __device__ __forceinline__ float2 value(int s) const {
     if (a.lg_field) {  // dL/dE = 2 E dL/dI, dL/dI = g (r / m - [argmax] S / m^2) (mse_backward_kernel)
       const float2 e = lg_row[s];
       const float I = loss_intensity(e);
@@ -280,7 +293,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
   // planes start at plane zoff * BC of `in`
   const int plane = row / a.Hin, h = row - plane * a.Hin;
   float2* dst = T + (size_t)plane * a.ncb * CB * a.Hin;
-  const RowSrc fetch(a, in, plane, h);
+  const RowSrc<false> fetch(a, in, plane, h);
   if constexpr (PN > 0 && !is_mx(PN)) {
     // twiddle-table loads first, their LDS writes after the row loads (as in K3)
     constexpr int TT = Geo<PN>::T;
@@ -1286,7 +1299,7 @@ asm_rows_fwd_m3(const float2* __restrict__ in, float2* __restrict__ T, FftPlan p
   const bool live = row < rows;
   const int rw = live ? row : rows - 1;
   const int plane = rw / a.Hin, hr = rw - plane * a.Hin;
-  const RowSrc fetch(a, in, plane, hr);
+  const RowSrc<true> fetch(a, in, plane, hr);
   float2* rowbuf = lds + h * M3_L;
   if (live && act) {
 #pragma unroll
@@ -1389,7 +1402,8 @@ asm_rows_inv_m3(const float2* __restrict__ U, float2* __restrict__ out, FftPlan 
     if (rr >= rows) continue;
     const int pl = rr / a.Hout, rout = rr - pl * a.Hout;
     const float2* s0 = lds + 3 * hh * M3_IMS + w;
-    const float2 v = cadd(cadd(s0[0], s0[M3_IMS]), s0[2 * M3_IMS]);  // (1 / (Ph Pw) applied by K2)
+    float2 v = cadd(cadd(s0[0], s0[M3_IMS]), s0[2 * M3_IMS]);  // (1 / (Ph Pw) applied by K2)
+    if (a.ap_side == 1 && !aperture_open(a.apm, rout, w)) v = cscale(v, 0.f);  // window mask (forward)
     out[((size_t)(a.zoff * a.BC + pl) * a.Hout + rout) * a.Wout + w] = v;
     if constexpr (LOSS) {
       const int lb = pl / a.C, lc = pl - lb * a.C;
@@ -2119,6 +2133,21 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
     a.mod_tand = m->tand;
     a.mod_rng = m->rng;
     a.mod_rng_stream = m->rng_stream;
+  }
+  if (d->window_mask) {
+    const thz_aperture_desc* w = d->window_mask;
+    if (w->kind != THZ_APERTURE_RECT && w->kind != THZ_APERTURE_CIRC)
+      return fail(THZ_E_ARG, "window mask: bad aperture kind %d", w->kind);
+    if (w->H != Ho || w->W != Wo)
+      return fail(THZ_E_ARG, "window mask %dx%d does not match the output grid %dx%d", w->H, w->W, Ho, Wo);
+    a.apm = aperture_args(w, Ho, Wo);
+    a.ap_side = d->adjoint ? 2 : 1;
+    // carried by the 300-point layer passes only (asm_rows_inv_m3 stores, asm_rows_fwd_m3 loads)
+    if (d->adjoint ? !k1_m3(g.Pw, a) : !k3_m3(g.Pw, a))
+      return fail(THZ_E_UNSUPPORTED, "window mask: only the 300-point layer geometry (100-pixel windows, "
+                                     "padding 2) folds the aperture; apply it separately");
+    if (d->adjoint && d->Z > 1)
+      return fail(THZ_E_UNSUPPORTED, "window mask: one z-plane per adjoint call");
   }
   if (ls) a.ls = *ls;
   if (lg_field) {  // the adjoint pipeline starts from the loss gradient

@@ -84,6 +84,34 @@ __device__ __forceinline__ float2 cis_d(double ph) {
 
 __device__ __forceinline__ int freq_index(int i, int n) { return i < n - n / 2 ? i : i - n; }
 
+// Aperture masks (Components/Aperture.py:44-136): the aperture kernel and the ASM window mask
+// (thz_asm_desc.window_mask) evaluate the same test.
+struct ApertureArgs {
+  int BC, H, W, kind;  // THZ_APERTURE_*
+  float ax0, ax1, ay0, ay1;  // linspace end points of the two grid axes
+  float half_w, half_h, radius;
+};
+
+__host__ __device__ inline ApertureArgs aperture_args(const thz_aperture_desc* d, int H, int W) {
+  ApertureArgs a{};
+  a.BC = d->BC; a.H = H; a.W = W; a.kind = d->kind;
+  if (d->kind == THZ_APERTURE_RECT) {
+    a.ax0 = (-d->dx * (float)W) / 2.0f;  // x over W with dx (Aperture.py:115)
+    a.ax1 = (d->dx * (float)W) / 2.0f;
+    a.ay0 = (-d->dy * (float)H) / 2.0f;  // y over H with dy (:116)
+    a.ay1 = (d->dy * (float)H) / 2.0f;
+  } else {
+    a.ax0 = (-d->dx * (float)H) / 2.0f;  // x over H with dx (:76)
+    a.ax1 = (d->dx * (float)H) / 2.0f;
+    a.ay0 = (-d->dy * (float)W) / 2.0f;
+    a.ay1 = (d->dy * (float)W) / 2.0f;
+  }
+  a.half_w = d->half_w;
+  a.half_h = d->half_h;
+  a.radius = d->radius;
+  return a;
+}
+
 // RS kernel exp(ikr) z/(2 pi r^2) (1/r - ik) (Props/CZT_Prop.py:44-57).  The amplitude is
 // fp32 in the reference's operation order; the phase k r (thousands of radians) is formed as
 // (k|z| mod 2 pi, from double) + k rho^2 / (r + |z|) -- the exact identity r - |z| =
@@ -157,6 +185,18 @@ __device__ __forceinline__ float lin(float start, float end, int n, int i) {
   const float step = (end - start) / (float)(n - 1);
   const bool lo = i < n / 2;
   return (lo ? start : end) + step * (float)(lo ? i : i - (n - 1));
+}
+
+// pixel (i, j) of an H x W field open under the aperture (the reference's grids and fp32 tests)
+__device__ __forceinline__ bool aperture_open(const ApertureArgs& a, int i, int j) {
+  if (a.kind == THZ_APERTURE_RECT) {
+    // meshgrid(x over W, y over H, indexing='xy'): X[i, j] = x[j], Y[i, j] = y[i]
+    const float X = lin(a.ax0, a.ax1, a.W, j), Y = lin(a.ay0, a.ay1, a.H, i);
+    return fabsf(X) <= a.half_w && fabsf(Y) <= a.half_h;
+  }
+  // circ: meshgrid(x over H, y over W) 'ij'
+  const float X = lin(a.ax0, a.ax1, a.H, i), Y = lin(a.ay0, a.ay1, a.W, j);
+  return sqrtf(X * X + Y * Y) <= a.radius;
 }
 #pragma clang fp contract(on)
 

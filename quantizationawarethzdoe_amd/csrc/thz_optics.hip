@@ -71,23 +71,6 @@ __global__ void __launch_bounds__(EW_THREADS) thin_lens_kernel(const float2* __r
   });
 }
 
-struct ApertureArgs {
-  int BC, H, W, kind;  // THZ_APERTURE_*
-  float ax0, ax1, ay0, ay1;  // linspace end points of the two grid axes
-  float half_w, half_h, radius;
-};
-
-__device__ __forceinline__ bool aperture_open(const ApertureArgs& a, int i, int j) {
-  if (a.kind == THZ_APERTURE_RECT) {
-    // meshgrid(x over W, y over H, indexing='xy'): X[i, j] = x[j], Y[i, j] = y[i]
-    const float X = lin(a.ax0, a.ax1, a.W, j), Y = lin(a.ay0, a.ay1, a.H, i);
-    return fabsf(X) <= a.half_w && fabsf(Y) <= a.half_h;
-  }
-  // circ: meshgrid(x over H, y over W) 'ij'
-  const float X = lin(a.ax0, a.ax1, a.H, i), Y = lin(a.ay0, a.ay1, a.W, j);
-  return sqrtf(X * X + Y * Y) <= a.radius;
-}
-
 // the mask as a complex factor (1 or 0), evaluated once per pixel: NaN / inf propagate as in the
 // reference's product field * mask
 __global__ void __launch_bounds__(EW_THREADS) aperture_kernel(const float2* __restrict__ in,
@@ -436,22 +419,7 @@ extern "C" int thz_aperture(const thz_aperture_desc* d, const void* in, void* ou
   if (!d || !in || !out || d->BC < 1 || d->H < 1 || d->W < 1) return fail(THZ_E_ARG, "bad aperture arguments");
   if (d->kind != THZ_APERTURE_RECT && d->kind != THZ_APERTURE_CIRC)
     return fail(THZ_E_ARG, "bad aperture kind %d", d->kind);
-  ApertureArgs a{};
-  a.BC = d->BC; a.H = d->H; a.W = d->W; a.kind = d->kind;
-  if (d->kind == THZ_APERTURE_RECT) {
-    a.ax0 = (-d->dx * (float)d->W) / 2.0f;  // x over W with dx (Aperture.py:115)
-    a.ax1 = (d->dx * (float)d->W) / 2.0f;
-    a.ay0 = (-d->dy * (float)d->H) / 2.0f;  // y over H with dy (:116)
-    a.ay1 = (d->dy * (float)d->H) / 2.0f;
-  } else {
-    a.ax0 = (-d->dx * (float)d->H) / 2.0f;  // x over H with dx (:76)
-    a.ax1 = (d->dx * (float)d->H) / 2.0f;
-    a.ay0 = (-d->dy * (float)d->W) / 2.0f;
-    a.ay1 = (d->dy * (float)d->W) / 2.0f;
-  }
-  a.half_w = d->half_w;
-  a.half_h = d->half_h;
-  a.radius = d->radius;
+  const ApertureArgs a = aperture_args(d, d->H, d->W);
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("aperture", s);
   const int n = d->H * d->W;

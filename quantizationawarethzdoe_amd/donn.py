@@ -45,6 +45,32 @@ def default_params():
     return doe_params, optim_params
 
 
+def propagate_through_aperture(prop, aperture, field):
+    """``aperture(prop(field))`` -- an ASM_prop to one plane, then an ApertureElement -- with the
+    aperture folded into the propagation when the library carries it (thz_asm_desc.window_mask:
+    the 300-point layer geometry): the row-inverse pass stores the masked field and the backward's
+    row pass masks the incoming gradient, so no aperture kernel runs either way.  Otherwise (other
+    geometries, complex128, a multi-valued z, deferred output) the two modules run as written."""
+    B, C, H, W = field.shape
+    ph, pw = prop.compute_padding(H, W, return_size_of_padding=True)
+    unpad = (not prop.do_padding) or prop.do_unpad_after_pad
+    if field._pending is not None and field._take_pending() is None:  # a deferred propagation's output
+        return aperture(prop(field))
+    pend = field._take_pending()  # the DOE layer's unevaluated modulation, or None
+    data = pend.field if pend is not None else field.data
+    dt = _prop.kernel_dtype(data, "ASM_prop", field.wavelengths).dtype
+    if (dt != torch.complex64 or len(prop._zh) != 1 or _prop.deferring()
+            or not _prop.window_mask_fusable(H, W, ph, pw, unpad)):
+        return aperture(prop(field))
+    mask = aperture.window_desc(field, H, W)
+    if mask is None:
+        return aperture(prop(field))
+    out = prop._run(field, prop._zh, out_mask=mask).squeeze(0)
+    aperture._note_input(field, shape=out.shape, dtype=out.dtype)
+    return ElectricField(data=out, wavelengths=field.wavelengths, spacing=field.spacing,
+                         device=field.device)._adopt_host(field)
+
+
 class DONN(nn.Module):
     def __init__(self, input_dxy=1 * mm, input_field_shape=(100, 100), doe_params=None, optim_params=None,
                  wavelengths=C0 / 300e9, num_layer=3, d_layer=20 * mm, q_method=None, device=None):
@@ -90,15 +116,14 @@ class DONN(nn.Module):
         u = u.to(self.device)
         field = ElectricField(data=u.to(torch.complex64), wavelengths=self._tmpl.wavelengths,
                               spacing=self._tmpl.spacing, device=self.device)._adopt_host(self._tmpl)
-        return self.aperture(self.asm_prop2layer(field))
+        return propagate_through_aperture(self.asm_prop2layer, self.aperture, field)
 
     def forward(self, u, iter_frac=None, chained=False):
         inputs = self.encode_object(u)
         field = inputs
         for i in range(self.num_layer - 1):
             field = self.does[i](field if chained else inputs, iter_frac)
-            field = self.asm_prop_layer(field)
-            field = self.aperture(field)
+            field = propagate_through_aperture(self.asm_prop_layer, self.aperture, field)
         field = self.does[-1](field if chained else inputs, iter_frac)
         return self.asm_prop2detector(field)
 

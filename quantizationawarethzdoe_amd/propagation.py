@@ -11,6 +11,7 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
+import os
 import threading
 
 import torch
@@ -51,20 +52,30 @@ def asm_padding(H, W, padding_scale, do_padding=True):
     return int(math.floor(float(sh) * H / 2)), int(math.floor(float(sw) * W / 2))
 
 
-def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk=0):
+def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk=0,
+              mask=None):
+    """thz_asm_desc; ``mask``: an ApertureDesc on the output grid (thz_asm_desc.window_mask)."""
     wl = _lib.float_array(wavelengths)
     zv = _lib.float_array(zs)
     d = _lib.AsmDesc(B=B, C=C, H=H, W=W, pad_h=pad_h, pad_w=pad_w, unpad=int(bool(unpad)),
                      bandlimit=int(bandlimit), Z=len(zs), adjoint=int(adjoint), z_chunk=int(z_chunk),
                      dx=float(spacing[0]), dy=float(spacing[1]),
                      wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
-                     z=ctypes.cast(zv, ctypes.POINTER(ctypes.c_float)))
-    d._keep = (wl, zv)
+                     z=ctypes.cast(zv, ctypes.POINTER(ctypes.c_float)),
+                     window_mask=ctypes.addressof(mask) if mask is not None else None)
+    d._keep = (wl, zv, mask)
     return d
 
 
+def window_mask_fusable(H, W, pad_h, pad_w, unpad, Z=1):
+    """True when the library folds an aperture into the propagation (thz_asm_desc.window_mask): the
+    300-point layer geometry of the cfg4 / cfg5 systems (100-pixel fields, padding 2, cropped)."""
+    return (H == W == 100 and pad_h == pad_w == 100 and bool(unpad) and Z == 1
+            and os.environ.get("THZ_K2_M3", "1") != "0")
+
+
 def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint=False, z_chunk=0,
-              out=None):
+              out=None, mask=None):
     """Raw launch: forward data [B,C,H,W] -> [Z,B,C,Ho,Wo]; adjoint [Z,B,C,Ho,Wo] -> [B,C,H,W], the sum
     over the Z planes of each plane's adjoint (one pipeline: the column pass sums the planes'
     spectra, thz_asm_forward with adjoint = 1)."""
@@ -86,7 +97,7 @@ def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, ad
         B, C, H, W = data.shape
         Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
         out_shape = (len(zs), B, C, Ho, Wo)
-    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk)
+    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk, mask)
     nbytes = ctypes.c_size_t(0)
     _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
     ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
@@ -156,16 +167,17 @@ def asm_band_columns(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, sp
 
 class _AsmFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_chunk):
-        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit)
-        return asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, False, z_chunk)
+    def forward(ctx, data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_chunk, mask):
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask)
+        return asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, False, z_chunk, mask=mask)
 
     @staticmethod
     def backward(ctx, g):
-        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
-        # one adjoint launch for all planes: sum_z A_z^H g_z, the sum taken in the column pass
-        gin = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
-        return gin, None, None, None, None, None, None, None, None
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask = ctx.cfg
+        # one adjoint launch for all planes: sum_z A_z^H g_z, the sum taken in the column pass (the
+        # window mask, when folded, on the adjoint's input)
+        gin = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask)
+        return gin, None, None, None, None, None, None, None, None, None
 
 
 def asm_transfer_function(wavelengths, spacing, z, H, W, pad_h, pad_w, bandlimit, device):
@@ -203,11 +215,13 @@ def rs_kernel(meshx, meshy, z, wavelengths):
     return out
 
 
-def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", z_chunk=0):
-    """Differentiable ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo] (HIP kernels)."""
+def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", z_chunk=0,
+                  mask=None):
+    """Differentiable ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo] (HIP kernels); ``mask``: an
+    aperture folded onto the output (window_mask_fusable geometry only)."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
     return _AsmFunction.apply(data, list(map(float, wavelengths)), tuple(map(float, spacing)),
-                              list(map(float, zs)), int(pad_h), int(pad_w), bool(unpad), bl, int(z_chunk))
+                              list(map(float, zs)), int(pad_h), int(pad_w), bool(unpad), bl, int(z_chunk), mask)
 
 
 class _AsmModulatedFunction(torch.autograd.Function):
@@ -216,13 +230,13 @@ class _AsmModulatedFunction(torch.autograd.Function):
     (one launch), then the modulate backward kernel (grad_field, grad_height)."""
 
     @staticmethod
-    def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
+    def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask):
         _require_device(field, "ASM")
         field = field.contiguous()
         h = height.detach().contiguous().float()
         B, C, H, W = field.shape
         Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
-        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False)
+        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False, mask=mask)
         m = pend.desc()
         L = _lib.lib()
         nbytes = ctypes.c_size_t(0)
@@ -241,7 +255,7 @@ class _AsmModulatedFunction(torch.autograd.Function):
             pend.hfull = hfull
         ctx.save_for_backward(field, h)
         ctx.pend = pend
-        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit)
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask)
         return out
 
     @staticmethod
@@ -249,19 +263,20 @@ class _AsmModulatedFunction(torch.autograd.Function):
         from . import doe as _doe
         field, h = ctx.saved_tensors
         pend = ctx.pend
-        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
-        gm = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask = ctx.cfg
+        gm = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask)
         gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
                                         ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
-        return gf, gh, None, None, None, None, None, None, None, None
+        return gf, gh, None, None, None, None, None, None, None, None, None
 
 
-def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact"):
-    """Differentiable fused DOE modulation + ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo]."""
+def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", mask=None):
+    """Differentiable fused DOE modulation + ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo]; ``mask``
+    as asm_propagate."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
     return _AsmModulatedFunction.apply(pend.field, pend.height, pend, list(map(float, wavelengths)),
                                        tuple(map(float, spacing)), list(map(float, zs)), int(pad_h), int(pad_w),
-                                       bool(unpad), bl)
+                                       bool(unpad), bl, mask)
 
 
 class _AsmLossFunction(torch.autograd.Function):
