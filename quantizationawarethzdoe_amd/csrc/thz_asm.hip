@@ -647,9 +647,10 @@ constexpr int TINV = 15 * 64;  // w1024^(lane c), [c - 1][lane]
 constexpr int T64 = 3 * 16;    // w64^(g e), [g - 1][e]
 constexpr int TW8 = 64 + 16;   // w8192^n2 = w8192^(n2 & 63) w128^(n2 >> 6), n2 < 1024
 static_assert(IMG >= 8 * SL && IMG >= lds_floats2(N), "slice region");
-__host__ __device__ constexpr size_t lds_bytes(int nz) {
-  return (size_t)(IMG + TINV + T64 + TW8) * sizeof(float2) + 4 * nz;
+__host__ __device__ constexpr size_t lds_bytes(int nz, int nc = 1) {
+  return (size_t)(nc * IMG + TINV + T64 + TW8) * sizeof(float2) + 4 * nc * nz;
 }
+static_assert(lds_bytes(THZ_MAX_Z, 2) <= 160 * 1024, "paired four-step K2 LDS");
 }  // namespace fs
 
 __device__ __forceinline__ void swap_rows16(float& a, float& b) {
@@ -709,14 +710,20 @@ __device__ __forceinline__ void wave_ifft1024(float2 (&x)[16], int lane, float2*
   dft16<true>(x);  // x[h] = output lane + 64 h
 }
 
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+// NC = 2 (asm_cols_4s_pair, opt-in THZ_K2_4S=2): two 512-thread halves run columns 2p and 2p + 1
+// of one U block in lockstep (same barriers), each on its own slice image; the tables are shared.
+// The pair's U rows fill 16 of each 32-B sector from one workgroup instead of 8 (the round-3
+// asm_cols_pair experiment: U writes exact), at one 16-wave workgroup per CU.
+template <int NC>
+__device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                 const AsmArgs& a) {
   constexpr int PN = fs::N, TT = fs::T;
-  extern __shared__ float2 lds[];
-  float2* const tinv = lds + fs::IMG;
+  extern __shared__ float2 lds_all[];
+  const int half = NC == 2 ? (int)(threadIdx.x >> 9) : 0;
+  float2* const lds = lds_all + half * fs::IMG;
+  float2* const tinv = lds_all + NC * fs::IMG;
   float2* const t64 = tinv + fs::TINV;
   float2* const tw8 = t64 + fs::T64;
-  int* const mz = reinterpret_cast<int*>(tw8 + fs::TW8);
   int id, z_lo = 0, z_hi = a.nz;
   if ((int)blockIdx.x < a.kfull) {
     id = xcd_chunk(blockIdx.x, a.kfull);
@@ -726,15 +733,21 @@ asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, As
     z_lo = part * a.nz / a.kparts;
     z_hi = (part + 1) * a.nz / a.kparts;
   }
-  const int bc = id / a.ncols, c = id - bc * a.ncols;
+  int* const mz = reinterpret_cast<int*>(tw8 + fs::TW8) + half * (z_hi - z_lo);
+  const int ncp = (a.ncols + NC - 1) / NC;
+  const int bc = id / ncp, cp = NC * (id - bc * ncp) + half;
+  const bool live = cp < a.ncols;  // an odd last column: the partner half runs for the barriers only
+  const int c = live ? cp : a.ncols - 1;
   const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
   const float lam = a.lam[bc % a.C];
   const float Ky = kfreq(c - a.J, a.Pw, a.dy);
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x & (TT - 1), lane = tid & 63, w = tid >> 6;
   const float2* __restrict__ tw = ph.tw;  // exp(-2 pi i t / 8192)
-  for (int i = tid; i < fs::TINV; i += TT) tinv[i] = tw[8 * (i & 63) * ((i >> 6) + 1)];
-  if (tid < fs::T64) t64[tid] = tw[128 * ((tid >> 4) + 1) * (tid & 15)];
-  if (tid < fs::TW8) tw8[tid] = tw[tid < 64 ? tid : 64 * (tid - 64)];
+  if (half == 0) {
+    for (int i = tid; i < fs::TINV; i += TT) tinv[i] = tw[8 * (i & 63) * ((i >> 6) + 1)];
+    if (tid < fs::T64) t64[tid] = tw[128 * ((tid >> 4) + 1) * (tid & 15)];
+    if (tid < fs::TW8) tw8[tid] = tw[tid < 64 ? tid : 64 * (tid - 64)];
+  }
   // kept rows |m_x| <= M_z per z (bisection with the reference-order tests, as asm_cols)
   {
     for (int zz = tid; zz < z_hi - z_lo; zz += TT) {
@@ -836,10 +849,20 @@ asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, As
       for (int n1 = 0; n1 < 8; ++n1) {
         const int r = 1024 * n1 + n2 - a.out_r0;
         // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2)
-        if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v[n1];
+        if (live && (unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v[n1];
       }
     }
   }
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_4s_body<1>(T, U, ph, a);
+}
+
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+asm_cols_4s_pair(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_4s_body<2>(T, U, ph, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1766,6 +1789,10 @@ static int ensure_lds_attr() {
     const hipError_t e4 = hipFuncSetAttribute((const void*)asm_cols_4s, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)fs::lds_bytes(THZ_MAX_Z));
     if (e4 != hipSuccess) err = e4;
+    const hipError_t e6 = hipFuncSetAttribute((const void*)asm_cols_4s_pair,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)fs::lds_bytes(THZ_MAX_Z, 2));
+    if (e6 != hipSuccess) err = e6;
     const hipError_t e5 = hipFuncSetAttribute((const void*)asm_rows_inv_4s,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3_4s_lds_bytes());
     if (e5 != hipSuccess) err = e5;
@@ -1799,13 +1826,15 @@ static bool k2_pair(int Ph) {
   return on && Ph == 8192;
 }
 // Four-step K2 (asm_cols_4s) at Ph = 8192 for the analytic transfer function (ASM forward and
-// adjoint of one z-chunk); THZ_K2_4S=0 selects the three-stage asm_cols (A/B switch).
-static bool k2_4s(int Ph, const AsmArgs& a) {
-  static const bool on = [] {
+// adjoint of one z-chunk); THZ_K2_4S=0 selects the three-stage asm_cols, THZ_K2_4S=2 the paired
+// asm_cols_4s_pair (A/B switches).  Returns 0 (off), 1 or 2 (columns per workgroup).
+static int k2_4s(int Ph, const AsmArgs& a) {
+  static const int mode = [] {
     const char* e = getenv("THZ_K2_4S");
-    return !(e && e[0] == '0');
+    if (!e) return 1;
+    return e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1;
   }();
-  return on && Ph == fs::N && !a.tft && !a.zsum;
+  return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
 }
 // Four-step K3 (asm_rows_inv_4s) at Pw = 8192, opt-in THZ_K3_4S=1 (A/B against asm_rows_inv<8192>).
 static bool k3_4s(int Pw) {
@@ -2007,11 +2036,15 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
-      } else if (k2_4s(g.Ph, a)) {
+      } else if (const int nc4 = k2_4s(g.Ph, a)) {
         // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
-        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z));
-        const int ntask = k2_tasks(g, &a, fs::T, lds2, false, (const void*)asm_cols_4s);
-        hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
+        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z), nc4);
+        const void* kern = nc4 == 2 ? (const void*)asm_cols_4s_pair : (const void*)asm_cols_4s;
+        const int ntask = k2_tasks(g, &a, nc4 * fs::T, lds2, nc4 == 2, kern);
+        if (nc4 == 2)
+          hipLaunchKernelGGL(asm_cols_4s_pair, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
+        else
+          hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_pair(g.Ph)) {
         const size_t lds2 = k2_pair_lds(g.Ph);
         const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);

@@ -274,8 +274,12 @@ __device__ __forceinline__ float rng_u01(const unsigned* rng, unsigned stream, u
   return (float)(unsigned)(rng_bits(rng, stream, idx) >> 40) * (1.0f / 16777216.0f);
 }
 // Exp(1) = -log U with U in (0, 1] (Tensor.exponential_)
+// Exp(1) = -log(u), u = (b + 1) / 2^24 in (0, 1].  The top bin (u = 1, probability 2^-24) gives
+// E = 0 and a Gumbel draw -log(E) = +inf, which turns gumbel_softmax into NaN (a 6,000-iteration
+// v3 / naive-Gumbel run draws ~10^7-10^8 values): E is held at 2^-25, the middle of that bin's range.
 __device__ __forceinline__ float rng_exp1(const unsigned* rng, unsigned stream, unsigned idx) {
-  return -logf((float)((unsigned)(rng_bits(rng, stream, idx) >> 40) + 1u) * (1.0f / 16777216.0f));
+  const float e = -logf((float)((unsigned)(rng_bits(rng, stream, idx) >> 40) + 1u) * (1.0f / 16777216.0f));
+  return fmaxf(e, 2.98023224e-8f);
 }
 
 // noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85); u == nullptr: the device

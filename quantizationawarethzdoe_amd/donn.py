@@ -24,7 +24,7 @@ import torch
 import torch.nn as nn
 
 from quantizationawarethzdoe_amd import optics as _optics
-from quantizationawarethzdoe_amd.qat import _CAPTURE_MODE
+from quantizationawarethzdoe_amd.qat import _CAPTURE_MODE, agreed_capture, release_step_graph
 from quantizationawarethzdoe_amd import propagation as _prop
 from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
 from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
@@ -207,7 +207,6 @@ class DONNTrainer:
         loss = self._loss(u, target, frac)
         # preallocated d loss / d loss: no fill kernel per step
         loss.backward(gradient=self._one if loss.dtype == self._one.dtype and loss.device == self._one.device else None)
-        from quantizationawarethzdoe_amd.qat import release_step_graph
         release_step_graph([self.model])
         self.allreduce.pack()
         # detached: the returned (graph-static) loss must not hold the step's autograd graph, whose
@@ -237,6 +236,9 @@ class DONNTrainer:
 
     # -- graph path ----------------------------------------------------------------------------
     def _capture(self, frac):
+        # a graph left by construction or by eager steps (the layers' attached height maps) would
+        # hand the warm-up the weights' AccumulateGrad nodes made on another stream
+        release_step_graph([self.model])
         su, st = self._static
         p0 = [p.detach().clone() for p in self.params]
         st0 = {id(p): {k: v.clone() for k, v in self.optimizer.state[p].items() if torch.is_tensor(v)}
@@ -263,7 +265,6 @@ class DONNTrainer:
             self.optimizer.zero_grad(set_to_none=True)
             if not self.allreduce.active or (self.capture_collective and self.allreduce.capturable):
                 # no collective, or a captured one: the whole step is one graph, one replay per step
-                from quantizationawarethzdoe_amd.qat import agreed_capture
 
                 def whole():
                     g = torch.cuda.CUDAGraph()

@@ -178,12 +178,23 @@ def release_step_graph(modules):
     autograd graph -- down to the weight's AccumulateGrad node -- alive until the next forward, so
     a HIP-graph capture would reuse the node its warm-up made on another stream (torch's
     "AccumulateGrad node's stream does not match" warning).  The values are
-    unchanged (a detached view of the same storage, which graph replays keep updating)."""
+    unchanged (a detached view of the same storage, which graph replays keep updating).  The same
+    for the layer's last pending modulation (its height, output and upsampled height map)."""
+    def _det(t):
+        return t.detach() if torch.is_tensor(t) and not isinstance(t, nn.Parameter) and t.grad_fn is not None else t
+
     for m in modules:
         for layer in m.modules():
             h = layer.__dict__.get("height_map")
-            if torch.is_tensor(h) and not isinstance(h, nn.Parameter) and h.grad_fn is not None:
-                layer.height_map = h.detach()
+            if torch.is_tensor(h):
+                layer.height_map = _det(h)
+            # the last modulation (DOELayer._height_map_ reads its hfull): its height and product
+            # tensors hold the same graph
+            pend = layer.__dict__.get("_pending_mod")
+            if pend is not None:
+                for k in ("field", "height", "out", "hfull"):
+                    if k in pend.__dict__:
+                        setattr(pend, k, _det(getattr(pend, k)))
 
 
 def agreed_capture(allreduce, capture_fn):
@@ -358,6 +369,9 @@ class QATTrainer:
 
     # -- graph path ----------------------------------------------------------------------------
     def _capture(self, frac):
+        # a graph left by construction (the layer's initial height map) or by eager steps would hand
+        # the warm-up the weights' AccumulateGrad nodes made on another stream
+        release_step_graph([self.system])
         params = self.allreduce.params
         # warm-up steps (allocator, autograd, Adam's lazy state) must not change the training
         # trajectory: snapshot the weights and the optimiser state, restore them afterwards

@@ -293,14 +293,16 @@ def test_asm_four_step_k2_matches_three_stage(tmp_path):
     """The four-step column pass (asm_cols_4s, the default at Ph = 8192: eight 1024-point wavefront
     transforms and one radix-8 step across the waves per z) against the three-stage asm_cols<8192>
     (THZ_K2_4S=0) on the cfg2 geometry: 7 planes over 20-120 mm (the kparts z-range split of the
-    last dispatch round included) and one adjoint plane.  Same transform, other rounding order:
-    rel-L2 <= 2e-6 (fp32 FFT rounding of an 8192-point transform pair)."""
+    last dispatch round included) and one adjoint plane; and the paired variant (THZ_K2_4S=2,
+    asm_cols_4s_pair: two columns per 1024-thread workgroup; the band's odd column count leaves
+    the last pair half-empty).  Same transform, other rounding order: rel-L2 <= 2e-6 (fp32 FFT
+    rounding of an 8192-point transform pair), for both four-step variants."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = []
-    for flag in ("1", "0"):
+    for flag in ("1", "0", "2"):
         path = str(tmp_path / f"k2_{flag}.npy")
         env = dict(os.environ, THZ_K2_4S=flag)
         r = subprocess.run([sys.executable, "-c", _K2_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
@@ -308,6 +310,7 @@ def test_asm_four_step_k2_matches_three_stage(tmp_path):
         assert r.returncode == 0, r.stderr[-2000:]
         res.append(np.load(path))
     assert rel_l2(res[0], res[1]) <= 2e-6
+    assert rel_l2(res[2], res[1]) <= 2e-6
 
 
 _M3_SCRIPT = r"""

@@ -85,7 +85,7 @@ def test_donn_captured_allreduce_matches_split_graphs(one_rank_rccl):
           f"captured {res[True][2]:.4f} ms")
 
 
-@pytest.mark.parametrize("which", ["qat", "donn"])
+@pytest.mark.parametrize("which", ["qat", "donn", "qat_full", "donn_eager_first"])
 def test_captured_trainers_keep_no_autograd_graph_alive(which):
     """the captured trainers used to keep a step's autograd graph alive (the DOE
     layer's attached ``height_map`` and the returned loss), so the next capture's backward reused
@@ -98,17 +98,28 @@ def test_captured_trainers_keep_no_autograd_graph_alive(which):
     torch.manual_seed(7)
     with warnings.catch_warnings(record=True) as rec:
         warnings.simplefilter("always")
-        if which == "qat":
-            system = qat.FourFocalSpotsSystem(device=dev)
+        if which.startswith("qat"):
+            if which == "qat_full":
+                # FullPrecisionDOELayer builds an attached height map in its constructor (the graph
+                # the capture's warm-up must not inherit)
+                from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+                dp, op = qat.default_params()
+                system = qat.FourFocalSpotsSystem(doe_class=Q.FullPrecisionDOELayer, optim_params=op, device=dev)
+            else:
+                system = qat.FourFocalSpotsSystem(device=dev)
             tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), max_itrs=100, graph=True)
             for frac in (0.1, 0.1, 0.5, 0.5, 0.9, 0.9):
                 loss = tr.step(frac)
             layers = [system.doe]
         else:
             model = donn.DONN(device=dev, q_method="sgs")
-            tr = donn.DONNTrainer(model, donn.detector_targets(device=dev), graph=True)
             u = torch.rand(4, 1, 100, 100, device=dev)
             lab = torch.randint(0, 10, (4,), device=dev)
+            if which == "donn_eager_first":
+                # eager steps on the default stream first (their graph must not reach the capture)
+                eager = donn.DONNTrainer(model, donn.detector_targets(device=dev), graph=False)
+                eager.step(u, lab, 0.1)
+            tr = donn.DONNTrainer(model, donn.detector_targets(device=dev), graph=True)
             for frac in (0.1, 0.1, 0.5, 0.5, 0.9, 0.9):
                 loss = tr.step(u, lab, frac)
             layers = list(model.does)
