@@ -307,7 +307,30 @@ def bench_qat(dev, rank, world, steps=60, dist=None):
     return {"workload": "cfg4: four_focal_spots QAT step (v3 DOE 100^2, ASM P=300, fused loss, Adam), "
                         "HIP-graph replay per schedule phase, gradient all-reduce over ranks (RCCL: inside the graph)",
             "graph_collective": bool(trainer.allreduce.capturable and trainer.capture_collective), "phases": out,
-            "output_check": check_qat(dev)}
+            "output_check": check_qat(dev), "quality_6000": qat_quality_6000(dev)}
+
+
+def qat_quality_6000(dev, seed=0, iters=6000):
+    """Outside the timed region: the notebook's whole v3 run (experiment_four_focal_spots.ipynb
+    cells 6-8: 6,000 iterations, iter_frac = itr / 6000, Adam lr 0.02) on this rank's GPU, its
+    final / minimum / last-100-mean loss against the reference's own curve
+    (plot_data/example_1/loss_curve_Ours.npy via tests/golden/qat_curves.json).  ok: the
+    last-100 mean and the minimum within [0.5x, 2x] of the reference's (tests/test_qat_quality_gpu.py;
+    scripts/qat_quality.py runs every method with five seeds)."""
+    import numpy as np
+    from quantizationawarethzdoe_amd import qat
+    with open(os.path.join(ROOT, "tests", "golden", "qat_curves.json")) as fh:
+        ref = json.load(fh)["methods"]["Ours"]
+    torch.manual_seed(seed)
+    system = qat.FourFocalSpotsSystem(device=dev)
+    trainer = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), lr=0.02, max_itrs=iters, graph=True)
+    curve, dt = trainer.train(iters, log_every=0)
+    c = curve.double().numpy()
+    st = {"final": float(c[-1]), "min": float(c.min()), "mean_last100": float(c[-100:].mean())}
+    ok = bool(np.all(np.isfinite(c)) and all(0.5 * ref[k] <= st[k] <= 2.0 * ref[k] for k in ("min", "mean_last100")))
+    return {"iterations": iters, "seconds": round(dt, 2), "ok": ok, **{k: float(f"{v:.4g}") for k, v in st.items()},
+            "reference": {k: float(f"{ref[k]:.4g}") for k in ("final", "min", "mean_last100")},
+            "reference_source": "plot_data/example_1/loss_curve_Ours.npy (tests/golden/qat_curves.json)"}
 
 
 def check_donn(dev, chained):

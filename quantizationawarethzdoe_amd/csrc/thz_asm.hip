@@ -1831,8 +1831,7 @@ static bool k2_pair(int Ph) {
 static int k2_4s(int Ph, const AsmArgs& a) {
   static const int mode = [] {
     const char* e = getenv("THZ_K2_4S");
-    if (!e) return 1;
-    return e[0] == '0' ? 0 : e[0] == '2' ? 2 : 1;
+    return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : 0;
   }();
   return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
 }
@@ -1850,7 +1849,7 @@ static bool k3_4s(int Pw) {
 static bool m3_on() {
   static const bool on = [] {
     const char* e = getenv("THZ_K2_M3");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

@@ -50,7 +50,7 @@ def propagate_through_aperture(prop, aperture, field):
     aperture folded into the propagation when the library carries it (thz_asm_desc.window_mask:
     the 300-point layer geometry): the row-inverse pass stores the masked field and the backward's
     row pass masks the incoming gradient, so no aperture kernel runs either way.  Otherwise (other
-    geometries, complex128, a multi-valued z, deferred output) the two modules run as written."""
+    geometries, complex128, a multi-valued z) the two modules run as written."""
     B, C, H, W = field.shape
     ph, pw = prop.compute_padding(H, W, return_size_of_padding=True)
     unpad = (not prop.do_padding) or prop.do_unpad_after_pad
@@ -59,7 +59,9 @@ def propagate_through_aperture(prop, aperture, field):
     pend = field._take_pending()  # the DOE layer's unevaluated modulation, or None
     data = pend.field if pend is not None else field.data
     dt = _prop.kernel_dtype(data, "ASM_prop", field.wavelengths).dtype
-    if (dt != torch.complex64 or len(prop._zh) != 1 or _prop.deferring()
+    # (inside the trainers' deferred_output block too: the aperture reads the propagation's output
+    # at once either way, so running it here defers nothing the loss fold needs)
+    if (dt != torch.complex64 or len(prop._zh) != 1
             or not _prop.window_mask_fusable(H, W, ph, pw, unpad)):
         return aperture(prop(field))
     mask = aperture.window_desc(field, H, W)
