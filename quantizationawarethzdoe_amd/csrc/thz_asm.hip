@@ -293,7 +293,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
   // planes start at plane zoff * BC of `in`
   const int plane = row / a.Hin, h = row - plane * a.Hin;
   float2* dst = T + (size_t)plane * a.ncb * CB * a.Hin;
-  const RowSrc<false> fetch(a, in, plane, h);
+  const RowSrc<is_mx(PN)> fetch(a, in, plane, h);  // the 300-point pass carries the adjoint's window mask
   if constexpr (PN > 0 && !is_mx(PN)) {
     // twiddle-table loads first, their LDS writes after the row loads (as in K3)
     constexpr int TT = Geo<PN>::T;
@@ -1479,6 +1479,8 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     ibase = (unsigned)((lc * a.Hout + r) * a.Wout);
   }
   auto put = [&](int w, float2 v) {
+    // the window mask of a folded aperture (forward): the 300-point pass only
+    if constexpr (is_mx(PN)) if (a.ap_side == 1 && !aperture_open(a.apm, r, w)) v = cscale(v, 0.f);
     if constexpr (PN >= 1024 && !is_mx(PN)) {
       // large planes: written once and not read back by this pipeline, so streaming (non-temporal)
       // stores that do not displace the U lines the neighbouring rows' workgroups still gather
@@ -2174,10 +2176,11 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
       return fail(THZ_E_ARG, "window mask %dx%d does not match the output grid %dx%d", w->H, w->W, Ho, Wo);
     a.apm = aperture_args(w, Ho, Wo);
     a.ap_side = d->adjoint ? 2 : 1;
-    // carried by the 300-point layer passes only (asm_rows_inv_m3 stores, asm_rows_fwd_m3 loads)
-    if (d->adjoint ? !k1_m3(g.Pw, a) : !k3_m3(g.Pw, a))
-      return fail(THZ_E_UNSUPPORTED, "window mask: only the 300-point layer geometry (100-pixel windows, "
-                                     "padding 2) folds the aperture; apply it separately");
+    // carried by the 300-point row passes only (the K3 storer forward, the K1 loader adjoint:
+    // asm_rows_inv<300> / asm_rows_fwd<300>, or their 3 x 100 forms)
+    if (mx_kind(g.Pw) != Mx300::N && (d->adjoint ? !k1_m3(g.Pw, a) : !k3_m3(g.Pw, a)))
+      return fail(THZ_E_UNSUPPORTED, "window mask: only the 300-point row passes fold the aperture; "
+                                     "apply it separately");
     if (d->adjoint && d->Z > 1)
       return fail(THZ_E_UNSUPPORTED, "window mask: one z-plane per adjoint call");
   }

@@ -11,7 +11,6 @@ from __future__ import annotations
 import contextlib
 import ctypes
 import math
-import os
 import threading
 
 import torch
@@ -70,8 +69,7 @@ def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, 
 def window_mask_fusable(H, W, pad_h, pad_w, unpad, Z=1):
     """True when the library folds an aperture into the propagation (thz_asm_desc.window_mask): the
     300-point layer geometry of the cfg4 / cfg5 systems (100-pixel fields, padding 2, cropped)."""
-    return (H == W == 100 and pad_h == pad_w == 100 and bool(unpad) and Z == 1
-            and os.environ.get("THZ_K2_M3", "0") == "1")
+    return H == W == 100 and pad_h == pad_w == 100 and bool(unpad) and Z == 1
 
 
 def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint=False, z_chunk=0,

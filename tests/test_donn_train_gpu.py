@@ -156,15 +156,16 @@ print("ok")
 
 def test_aperture_folded_into_asm_matches_the_modules():
     """donn.propagate_through_aperture (the aperture as thz_asm_desc.window_mask: the 300-point row
-    pass multiplies its stores by the mask, the backward's row pass its loads; it rides on the 3 x
-    100 row passes, opt-in THZ_K2_M3=1, so it runs in a child process with that switch) ==
-    ApertureElement after ASM_prop, rect and circ, for a plain field and for a DOE layer's
-    unevaluated modulation: the same values bit for bit (v or v * 0), forward and gradients, and
-    the same .aperture attribute."""
+    pass multiplies its stores by the mask, the backward's row pass its loads) == ApertureElement
+    after ASM_prop, rect and circ, for a plain field and for a DOE layer's unevaluated modulation:
+    the same values bit for bit (v or v * 0), forward and gradients, and the same .aperture
+    attribute.  Both row-pass forms: the default 5 3 4 5 kernels and the opt-in 3 x 100 split
+    (THZ_K2_M3=1), each in a child process (the switch is read once per process)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    r = subprocess.run([sys.executable, "-c", _FOLD_SCRIPT.format(root=root)], env=dict(os.environ, THZ_K2_M3="1"),
-                       cwd=root, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-2000:]
+    for flag in ("0", "1"):
+        r = subprocess.run([sys.executable, "-c", _FOLD_SCRIPT.format(root=root)], env=dict(os.environ, THZ_K2_M3=flag),
+                           cwd=root, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0 and "ok" in r.stdout, (flag, r.stderr[-2000:])
