@@ -92,7 +92,9 @@ typedef struct thz_asm_desc {
    * applied in the row-inverse pass's stores (forward) or in the row pass's loads of the adjoint's
    * input (the adjoint of mask * ASM is ASM^H * mask).  Its BC is ignored; H, W must be the
    * output grid's (unpad ? H, W : the padded plane); the field is multiplied by 1 / 0, so NaN / inf
-   * propagate as in the reference's field * mask. */
+   * propagate as in the reference's field * mask.  Carried by the 300-point padded row length only
+   * (the DONN / QAT layer geometry); other geometries return THZ_E_UNSUPPORTED (apply
+   * thz_aperture separately), as does an adjoint with Z > 1. */
   const struct thz_aperture_desc* window_mask;
 } thz_asm_desc;
 
