@@ -1869,11 +1869,11 @@ static size_t k2_pair_lds(int Ph) {
 }
 static int k2_resident(int Ph, bool pair, int threads, size_t lds, const void* kern = nullptr) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, bool, const void*>, int> cache;
+  static std::map<std::tuple<int, int, bool, const void*, int, size_t>, int> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_tuple(dev, Ph, pair, kern);
+  auto key = std::make_tuple(dev, Ph, pair, kern, threads, lds);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const void* k = nullptr;
