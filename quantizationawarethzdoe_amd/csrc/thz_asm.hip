@@ -350,7 +350,10 @@ __device__ __forceinline__ int col_tid() {
   else return (int)threadIdx.x;
 }
 
-template <int PN, bool ZSUM, int NCOL = 1>
+// MID: the crop is the middle half of the padded column (out_r0 = PN / 4, Hout = PN / 2: padding
+// scale 1 with unpad, cfg2), a compile-time window, so the last stage's outputs outside it and
+// their store tests fold away.
+template <int PN, bool ZSUM, int NCOL = 1, bool MID = false>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
   static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
@@ -503,6 +506,10 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       const int M = mz[zz - z_lo];
       int tz = col_tid<PN, NCOL>();
       asm volatile("" : "+v"(tz));
+      // (the opaque copy hides the thread index's range: restate it, so that the band test below
+      // folds to one compare per element -- idx = tz + TT m + (PN / RL) r < PN / 2 is then known
+      // per (m, r) at compile time)
+      __builtin_assume(tz >= 0 && tz < TT);
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
       // the first stage's operands r in [4, 12) are the rows PN/4 <= |m_x| < 3 PN/4: when this
@@ -519,10 +526,10 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       };
       float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
-        const int r = j - a.out_r0;
+        const int r = j - (MID ? PN / 4 : a.out_r0);
         // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2;
         // streaming stores here ran K2 4.1 -> 13.8 ms)
-        if (live && (unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v;
+        if (live && (unsigned)r < (unsigned)(MID ? PN / 2 : a.Hout)) dst[(size_t)r * CBU] = v;
       };
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
     }
@@ -605,6 +612,12 @@ template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   asm_cols_body<PN, false>(T, U, ph, a);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols_mid(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
+                                                    AsmArgs a) {
+  asm_cols_body<PN, false, 1, true>(T, U, ph, a);
 }
 
 template <int PN>
@@ -1458,7 +1471,9 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
 // ---------------------------------------------------------------------------------------------
 // LOSS: the stored row also feeds the |E|^2 -> normalize -> MSE sums of its batch item
 // (LossAcc; Z == 1 so plane == bc), stored per workgroup in slot (c, r) of b by loss_store_part.
-template <int PN, bool LOSS>
+// MID: the crop is the middle half of the padded row (out_c0 = PN / 4, Wout = PN / 2: padding scale
+// 1 with unpad, cfg2), a compile-time window (as asm_cols_mid)
+template <int PN, bool LOSS, bool MID = false>
 __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw,
                                               const AsmArgs& a) {
   extern __shared__ float2 lds[];
@@ -1507,6 +1522,7 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     // stage's gather (the hook runs before the first exchange), so the gather does not wait behind
     // them: cfg2 K3 4.40 -> 4.28 ms (profiles/r03_k3_probes.txt)
     constexpr int TT = Geo<PN>::T;
+    __builtin_assume(tid >= 0 && tid < TT);  // the launch's block size: lets the crop test fold (MID)
     const auto twf = tw_fetch<PN, TT>(pw.tw, tid);
     const TwLds twl = tw_lds_at<PN>(tw_slot<PN>(lds));
     auto tw_hook = [&]() { tw_store<PN, TT>(tw_slot<PN>(lds), twf, tid); };
@@ -1531,8 +1547,8 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
       return base[(long)delta * a.Hout];
     };
     auto sv = [&](int, int, int j, float2 v) {
-      const int w = j - a.out_c0;
-      if ((unsigned)w < (unsigned)a.Wout) put(w, v);
+      const int w = j - (MID ? PN / 4 : a.out_c0);
+      if ((unsigned)w < (unsigned)(MID ? PN / 2 : a.Wout)) put(w, v);
     };
     fft_pow2_run<true, PN, TT, FFT_ROWS>(lds, twl, tid, ld, sv, tw_hook);
   } else {
@@ -1551,6 +1567,12 @@ template <int PN>
 __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv(const float2* __restrict__ U, float2* __restrict__ out,
                                                     FftPlan pw, AsmArgs a) {
   rows_inv_body<PN, false>(U, out, pw, a);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv_mid(const float2* __restrict__ U,
+                                                                      float2* __restrict__ out, FftPlan pw, AsmArgs a) {
+  rows_inv_body<PN, false, true>(U, out, pw, a);
 }
 
 template <int PN>
@@ -1759,6 +1781,10 @@ template <int PN>
 static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_rows_fwd<PN>);
   ks.push_back((const void*)asm_cols<PN>);
+  if constexpr (PN == 8192) {
+    ks.push_back((const void*)asm_cols_mid<PN>);
+    ks.push_back((const void*)asm_rows_inv_mid<PN>);
+  }
   ks.push_back((const void*)asm_cols_zsum<PN>);
   ks.push_back((const void*)asm_rows_inv<PN>);
   ks.push_back((const void*)asm_rows_inv_loss<PN>);
@@ -1836,6 +1862,23 @@ static int k2_4s(int Ph, const AsmArgs& a) {
     return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : 0;
   }();
   return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
+}
+// K2 at Ph = 8192 with the middle-half crop of padding scale 1 (cfg2): asm_cols_mid, the crop a
+// compile-time window (THZ_K2_MID=0 selects asm_cols<8192>, the A/B switch)
+static bool k2_mid(int Ph, const AsmArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K2_MID");
+    return !(e && e[0] == '0');
+  }();
+  return on && Ph == 8192 && !a.tft && !a.zsum && a.out_r0 == Ph / 4 && a.Hout == Ph / 2;
+}
+// K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid; THZ_K3_MID=0 selects asm_rows_inv<8192>)
+static bool k3_mid(int Pw, const AsmArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K3_MID");
+    return !(e && e[0] == '0');
+  }();
+  return on && Pw == 8192 && a.out_c0 == Pw / 4 && a.Wout == Pw / 2;
 }
 // Four-step K3 (asm_rows_inv_4s) at Pw = 8192, opt-in THZ_K3_4S=1 (A/B against asm_rows_inv<8192>).
 static bool k3_4s(int Pw) {
@@ -2050,6 +2093,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = k2_pair_lds(g.Ph);
         const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);
         hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
+      } else if (k2_mid(g.Ph, a)) {
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_mid<8192>);
+        hipLaunchKernelGGL(asm_cols_mid<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2);
@@ -2078,6 +2125,9 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
       } else if (k3_4s(g.Pw)) {
         hipLaunchKernelGGL(asm_rows_inv_4s, dim3((a.nz * g.BC * g.Hout + K3_RPW - 1) / K3_RPW), dim3(fs::T),
                            k3_4s_lds_bytes(), s, (const float2*)U, (float2*)out, pw, a);
+      } else if (k3_mid(g.Pw, a)) {
+        hipLaunchKernelGGL(asm_rows_inv_mid<8192>, dim3(a.nz * g.BC * g.Hout), dim3(threads_for(8192)),
+                           fft_lds_bytes_io(8192), s, (const float2*)U, (float2*)out, pw, a);
       } else {
         THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
                         (float2*)out, pw, a);

@@ -313,6 +313,27 @@ def test_asm_four_step_k2_matches_three_stage(tmp_path):
     assert rel_l2(res[2], res[1]) <= 2e-6
 
 
+def test_asm_middle_crop_kernels_match_the_generic_ones(tmp_path):
+    """cfg2's crop is the middle half of the padded plane (padding scale 1, unpad): asm_cols_mid /
+    asm_rows_inv_mid take it as a compile-time window, so the last stage's outputs outside it and
+    their store tests fold away.  Against asm_cols<8192> / asm_rows_inv<8192> (THZ_K2_MID=0,
+    THZ_K3_MID=0) on the cfg2 geometry, 7 planes and one adjoint plane: the kept outputs come
+    from the same operations, so the results are bit-identical."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for flag in ("1", "0"):
+        path = str(tmp_path / f"mid_{flag}.npy")
+        env = dict(os.environ, THZ_K2_MID=flag, THZ_K3_MID=flag)
+        r = subprocess.run([sys.executable, "-c", _K2_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(np.load(path))
+    np.testing.assert_array_equal(res[0], res[1])
+
+
 _M3_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, {root!r})
