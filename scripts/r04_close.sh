@@ -10,9 +10,9 @@ mkdir -p $o
 export TMPDIR=/tmp
 S=scripts/gpu_step.sh
 B="bench.py --steps 20 --warmup 5 --no-cpu-baseline --headline-only"
-bash $S 200 $o/mid_a.log python $B &&
+THZ_K2_MID=1 THZ_K3_MID=1 bash $S 200 $o/mid_a.log python $B &&
 THZ_K2_MID=0 THZ_K3_MID=0 bash $S 200 $o/gen_a.log python $B &&
-bash $S 200 $o/mid_b.log python $B &&
+THZ_K2_MID=1 THZ_K3_MID=1 bash $S 200 $o/mid_b.log python $B &&
 THZ_K2_MID=0 THZ_K3_MID=0 bash $S 200 $o/gen_b.log python $B || exit $?
 python3 - "$o" > $o/ab.txt <<'PY'
 import json, sys
@@ -26,7 +26,7 @@ gen = (v("gen_a") + v("gen_b")) / 2
 print(f"mid {mid:.1f} gen {gen:.1f} -> {'mid' if mid >= gen else 'generic'}")
 PY
 cat $o/ab.txt
-if grep -q "generic" $o/ab.txt; then export THZ_K2_MID=0 THZ_K3_MID=0; fi
+if grep -q "generic" $o/ab.txt; then export THZ_K2_MID=0 THZ_K3_MID=0; else export THZ_K2_MID=1 THZ_K3_MID=1; fi
 bash $S 1000 $o/gpu_tests.log python -u -m pytest tests -m gpu -q --timeout 240 --timeout-method thread -p no:cacheprovider &&
 bash $S 200 $o/smoke.log python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" &&
 bash $S 900 $o/prof.log bash scripts/profile_asm.sh $o/prof &&
