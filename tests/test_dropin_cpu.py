@@ -165,3 +165,57 @@ def test_czt_one_by_one_power_of_two_width_output_stays_in_the_graph():
     assert tuple(out.data.shape) == (1, 1, 1, 0)
     out.data.abs().sum().backward()
     assert x.grad is not None and float(x.grad.abs().sum()) == 0.0
+
+
+def test_release_step_graph_detaches_height_maps_and_pending_modulations():
+    """qat.release_step_graph: after a step (and before each capture) the DOE layers' last
+    ``height_map`` and their last pending modulation's tensors are detached -- same values, no
+    grad_fn -- so no autograd graph (and no weight AccumulateGrad node made on another stream)
+    outlives the step; parameters are left alone."""
+    import torch.nn as nn
+
+    from quantizationawarethzdoe_amd.qat import release_step_graph
+
+    class Pending:
+        pass
+
+    class Layer(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.weight = nn.Parameter(torch.randn(4, 4))
+
+        def forward(self):
+            self.height_map = torch.sigmoid(self.weight) * 2.0
+            p = Pending()
+            p.field = torch.randn(4, 4, dtype=torch.complex64)
+            p.height = self.height_map
+            p.out = self.height_map.to(torch.complex64) * p.field
+            p.hfull = self.height_map * 1.0
+            self._pending_mod = p
+            return p.out.abs().sum()
+
+    outer = nn.Sequential(Layer())
+    layer = outer[0]
+    layer().backward()
+    before = layer.height_map.detach().clone()
+    assert layer.height_map.grad_fn is not None and layer._pending_mod.out.grad_fn is not None
+    release_step_graph([outer])
+    assert layer.height_map.grad_fn is None and torch.equal(layer.height_map, before)
+    for k in ("height", "out", "hfull"):
+        assert getattr(layer._pending_mod, k).grad_fn is None, k
+    assert isinstance(layer.weight, nn.Parameter) and layer.weight.requires_grad
+
+
+def test_bench_strong_split_covers_the_64_plane_sweep_once():
+    """bench.z_planes: the strong split (--cfg2-split strong) hands the 64-plane cfg2 sweep to the
+    ranks, every plane exactly once and in order (8 per rank at N = 8); the weak split gives each
+    rank 64 planes of a 64 N sweep."""
+    import bench
+    for world in (1, 2, 3, 8):
+        parts = [bench.z_planes(r, world, "strong") for r in range(world)]
+        flat = [z for p in parts for z in p]
+        assert flat == bench.z_planes(0, 1, "strong") and len(flat) == bench.Z_PER_RANK
+        assert max(map(len, parts)) - min(map(len, parts)) <= 1
+        weak = [bench.z_planes(r, world, "weak") for r in range(world)]
+        assert all(len(p) == bench.Z_PER_RANK for p in weak)
+        assert len({z for p in weak for z in p}) == bench.Z_PER_RANK * world
