@@ -1864,7 +1864,8 @@ static int k2_4s(int Ph, const AsmArgs& a) {
   return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
 }
 // K2 at Ph = 8192 with the middle-half crop of padding scale 1 (cfg2): asm_cols_mid, the crop a
-// compile-time window (opt-in THZ_K2_MID=1 until measured on the box; A/B switch)
+// compile-time window: opt-in THZ_K2_MID=1 (measured 4.34-4.39 vs 4.19-4.22 ms on cfg2 with 10 % fewer
+// VALU instructions per plane: not the default)
 static bool k2_mid(int Ph, const AsmArgs& a) {
   static const bool on = [] {
     const char* e = getenv("THZ_K2_MID");
@@ -1872,11 +1873,12 @@ static bool k2_mid(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum && a.out_r0 == Ph / 4 && a.Hout == Ph / 2;
 }
-// K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid; opt-in THZ_K3_MID=1 until measured)
+// K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid, the default: 4.00 vs 4.13 ms on cfg2;
+// THZ_K3_MID=0 selects asm_rows_inv<8192>)
 static bool k3_mid(int Pw, const AsmArgs& a) {
   static const bool on = [] {
     const char* e = getenv("THZ_K3_MID");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on && Pw == 8192 && a.out_c0 == Pw / 4 && a.Wout == Pw / 2;
 }

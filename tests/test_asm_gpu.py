@@ -317,8 +317,10 @@ def test_asm_middle_crop_kernels_match_the_generic_ones(tmp_path):
     """cfg2's crop is the middle half of the padded plane (padding scale 1, unpad): asm_cols_mid /
     asm_rows_inv_mid take it as a compile-time window, so the last stage's outputs outside it and
     their store tests fold away.  Against asm_cols<8192> / asm_rows_inv<8192> (THZ_K2_MID=0,
-    THZ_K3_MID=0) on the cfg2 geometry, 7 planes and one adjoint plane: the kept outputs come
-    from the same operations, so the results are bit-identical."""
+    THZ_K3_MID=0) on the cfg2 geometry, 7 planes and one adjoint plane.  The kept outputs come from
+    the same butterflies, but the compiler schedules (and contracts) the folded code differently:
+    9.6 % of the elements differ by <= 2.4e-7 absolute on the box, so rel-L2 <= 2e-6 as for the
+    other transform variants."""
     import os
     import subprocess
     import sys
@@ -331,7 +333,7 @@ def test_asm_middle_crop_kernels_match_the_generic_ones(tmp_path):
                            capture_output=True, text=True, timeout=180)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append(np.load(path))
-    np.testing.assert_array_equal(res[0], res[1])
+    assert rel_l2(res[0], res[1]) <= 2e-6
 
 
 _M3_SCRIPT = r"""
