@@ -353,7 +353,7 @@ __device__ __forceinline__ int col_tid() {
 // MID: the crop is the middle half of the padded column (out_r0 = PN / 4, Hout = PN / 2: padding
 // scale 1 with unpad, cfg2), a compile-time window, so the last stage's outputs outside it and
 // their store tests fold away.
-template <int PN, bool ZSUM, int NCOL = 1, bool MID = false>
+template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = true>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
   static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
@@ -509,7 +509,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       // (the opaque copy hides the thread index's range: restate it, so that the band test below
       // folds to one compare per element -- idx = tz + TT m + (PN / RL) r < PN / 2 is then known
       // per (m, r) at compile time)
-      __builtin_assume(tz >= 0 && tz < TT);
+      if constexpr (RANGE) __builtin_assume(tz >= 0 && tz < TT);
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
       // the first stage's operands r in [4, 12) are the rows PN/4 <= |m_x| < 3 PN/4: when this
@@ -612,6 +612,13 @@ template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                 AsmArgs a) {
   asm_cols_body<PN, false>(T, U, ph, a);
+}
+
+// (A/B: asm_cols without the restated thread-index range, THZ_K2_RANGE=0)
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols_norange(const float2* __restrict__ T, float2* __restrict__ U,
+                                                        FftPlan ph, AsmArgs a) {
+  asm_cols_body<PN, false, 1, false, false>(T, U, ph, a);
 }
 
 template <int PN>
@@ -1783,6 +1790,7 @@ static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_cols<PN>);
   if constexpr (PN == 8192) {
     ks.push_back((const void*)asm_cols_mid<PN>);
+    ks.push_back((const void*)asm_cols_norange<PN>);
     ks.push_back((const void*)asm_rows_inv_mid<PN>);
   }
   ks.push_back((const void*)asm_cols_zsum<PN>);
@@ -1872,6 +1880,13 @@ static bool k2_mid(int Ph, const AsmArgs& a) {
     return e && e[0] == '1';
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum && a.out_r0 == Ph / 4 && a.Hout == Ph / 2;
+}
+static bool k2_norange(int Ph, const AsmArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K2_RANGE");
+    return e && e[0] == '0';
+  }();
+  return on && Ph == 8192 && !a.tft && !a.zsum;
 }
 // K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid, the default: 4.00 vs 4.13 ms on cfg2;
 // THZ_K3_MID=0 selects asm_rows_inv<8192>)
@@ -2095,6 +2110,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = k2_pair_lds(g.Ph);
         const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);
         hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
+      } else if (k2_norange(g.Ph, a)) {
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_norange<8192>);
+        hipLaunchKernelGGL(asm_cols_norange<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_mid(g.Ph, a)) {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_mid<8192>);
