@@ -353,7 +353,7 @@ __device__ __forceinline__ int col_tid() {
 // MID: the crop is the middle half of the padded column (out_r0 = PN / 4, Hout = PN / 2: padding
 // scale 1 with unpad, cfg2), a compile-time window, so the last stage's outputs outside it and
 // their store tests fold away.
-template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = true>
+template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = MID>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
   static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
@@ -506,9 +506,9 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       const int M = mz[zz - z_lo];
       int tz = col_tid<PN, NCOL>();
       asm volatile("" : "+v"(tz));
-      // (the opaque copy hides the thread index's range: restate it, so that the band test below
-      // folds to one compare per element -- idx = tz + TT m + (PN / RL) r < PN / 2 is then known
-      // per (m, r) at compile time)
+      // RANGE (asm_cols_range, asm_cols_mid): the opaque copy hides the thread index's range;
+      // restated, the band test below folds to one compare per element (idx = tz + TT m + (PN / RL) r
+      // < PN / 2 is then known per (m, r) at compile time), and with MID the crop's stores too
       if constexpr (RANGE) __builtin_assume(tz >= 0 && tz < TT);
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
@@ -614,11 +614,14 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
   asm_cols_body<PN, false>(T, U, ph, a);
 }
 
-// (A/B: asm_cols without the restated thread-index range, THZ_K2_RANGE=0)
+// A/B (opt-in THZ_K2_RANGE=1): asm_cols with the thread index's range restated, so the band test
+// folds to one compare per element (1316 -> 1241 VALU per thread per plane) -- but its reordered
+// stores merge worse in the L2 (U writes 1.9x instead of 1.6x) and it measured 4.18-4.19 vs
+// 4.06-4.08 ms on cfg2 (profiles/r04_experiments.txt)
 template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols_norange(const float2* __restrict__ T, float2* __restrict__ U,
-                                                        FftPlan ph, AsmArgs a) {
-  asm_cols_body<PN, false, 1, false, false>(T, U, ph, a);
+__global__ void __launch_bounds__(1024) asm_cols_range(const float2* __restrict__ T, float2* __restrict__ U,
+                                                      FftPlan ph, AsmArgs a) {
+  asm_cols_body<PN, false, 1, false, true>(T, U, ph, a);
 }
 
 template <int PN>
@@ -1790,7 +1793,7 @@ static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_cols<PN>);
   if constexpr (PN == 8192) {
     ks.push_back((const void*)asm_cols_mid<PN>);
-    ks.push_back((const void*)asm_cols_norange<PN>);
+    ks.push_back((const void*)asm_cols_range<PN>);
     ks.push_back((const void*)asm_rows_inv_mid<PN>);
   }
   ks.push_back((const void*)asm_cols_zsum<PN>);
@@ -1881,10 +1884,10 @@ static bool k2_mid(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum && a.out_r0 == Ph / 4 && a.Hout == Ph / 2;
 }
-static bool k2_norange(int Ph, const AsmArgs& a) {
+static bool k2_range(int Ph, const AsmArgs& a) {
   static const bool on = [] {
     const char* e = getenv("THZ_K2_RANGE");
-    return e && e[0] == '0';
+    return e && e[0] == '1';
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum;
 }
@@ -2110,10 +2113,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = k2_pair_lds(g.Ph);
         const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);
         hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
-      } else if (k2_norange(g.Ph, a)) {
+      } else if (k2_range(g.Ph, a)) {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_norange<8192>);
-        hipLaunchKernelGGL(asm_cols_norange<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
+        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_range<8192>);
+        hipLaunchKernelGGL(asm_cols_range<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_mid(g.Ph, a)) {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_mid<8192>);
