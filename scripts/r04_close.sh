@@ -4,7 +4,7 @@
 # line with the CPU baseline leg.  Each GPU step under its own time limit (gpu_step.sh).  (The
 # middle-crop A/B that first ran in this script: gpurun_out/close/ab.txt)
 set -o pipefail
-o=gpurun_out/close2
+o=gpurun_out/close3
 mkdir -p $o
 export TMPDIR=/tmp
 S=scripts/gpu_step.sh
