@@ -90,9 +90,6 @@ struct AsmArgs {
   // (adjoint input); apm is the mask on that grid
   int ap_side;
   ApertureArgs apm;
-  // K2 sibling pacing (opt-in THZ_K2_SYNC=1): per-column progress words, this launch's base value
-  int* sync_prog;
-  int sync_base;
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
@@ -504,30 +501,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
       return;
     }
-    // Sibling pacing (a.sync_prog, opt-in): the CBU column workgroups of a U block fill each
-    // 32-B sector of U together, and the L2 merges their writes only while they stay within about
-    // one plane of each other.  Each whole-column task publishes its plane index per z and, before
-    // plane zz, waits (bounded: PACE_SPIN sleeps, so an absent or late sibling costs time, never a
-    // hang) while a sibling that has started this launch is more than one plane behind.
-    const bool pace = NCOL == 1 && !ZSUM && a.sync_prog != nullptr && (int)blockIdx.x < a.kfull;
-    int* const prog = pace ? a.sync_prog + (size_t)bc * a.ncols : nullptr;
-    const int cb0 = c - c % CBU;
     for (int zz = z_lo; zz < z_hi; ++zz) {
-      if (pace) {
-        if (threadIdx.x == 0) {
-          __hip_atomic_store(prog + c, a.sync_base + zz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          for (int it = 0; it < 64; ++it) {  // PACE_SPIN
-            bool behind = false;
-            for (int k = cb0; k < cb0 + CBU && k < a.ncols; ++k) {
-              const int v = __hip_atomic_load(prog + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              behind |= v >= a.sync_base && v < a.sync_base + zz - 1;
-            }
-            if (!behind) break;
-            __builtin_amdgcn_s_sleep(8);
-          }
-        }
-        __syncthreads();
-      }
       const float z = a.zv[a.zoff + zz];
       const int M = mz[zz - z_lo];
       int tz = col_tid<PN, NCOL>();
@@ -1917,38 +1891,6 @@ static bool k2_range(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum;
 }
-// K2 sibling pacing (opt-in THZ_K2_SYNC=1, the default K2 at Ph = 8192 only): a per-device array
-// of per-column progress words, never reset -- each launch takes a fresh base (THZ_MAX_Z apart),
-// so words left by earlier launches read as "not started".  Returns nullptr when off or when the
-// allocation fails (the kernel then runs unpaced).
-static int* k2_sync_words(int Ph, const AsmGeom& g, int* base) {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K2_SYNC");
-    return e && e[0] == '1';
-  }();
-  if (!on || Ph != 8192) return nullptr;
-  static std::mutex mu;
-  static std::map<int, std::pair<int*, size_t>> bufs;
-  static int next = THZ_MAX_Z;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lk(mu);
-  const size_t n = (size_t)g.BC * g.ncols;
-  auto& b = bufs[dev];
-  if (b.second < n) {
-    if (b.first) (void)hipFree(b.first);
-    b = {nullptr, 0};
-    int* p = nullptr;
-    if (hipMalloc(&p, n * sizeof(int)) != hipSuccess || hipMemset(p, 0, n * sizeof(int)) != hipSuccess) {
-      if (p) (void)hipFree(p);
-      return nullptr;
-    }
-    b = {p, n};
-  }
-  *base = next;
-  next += THZ_MAX_Z;
-  return b.first;
-}
 // K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid, the default: 4.00 vs 4.13 ms on cfg2;
 // THZ_K3_MID=0 selects asm_rows_inv<8192>)
 static bool k3_mid(int Pw, const AsmArgs& a) {
@@ -2182,9 +2124,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2);
-        a.sync_prog = k2_sync_words(g.Ph, g, &a.sync_base);
         THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
-        a.sync_prog = nullptr;
       }
       THZ_LAUNCH_CHECK();
       kt.stop();
