@@ -673,7 +673,7 @@ static_assert(IMG >= 8 * SL && IMG >= lds_floats2(N), "slice region");
 __host__ __device__ constexpr size_t lds_bytes(int nz, int nc = 1) {
   return (size_t)(nc * IMG + TINV + T64 + TW8) * sizeof(float2) + 4 * nc * nz;
 }
-static_assert(lds_bytes(THZ_MAX_Z, 2) <= 160 * 1024, "paired four-step K2 LDS");
+static_assert(lds_bytes(THZ_MAX_Z, 2) + 8 <= 160 * 1024, "paired four-step K2 LDS (+ the HB counters)");
 }  // namespace fs
 
 __device__ __forceinline__ void swap_rows16(float& a, float& b) {
@@ -737,7 +737,21 @@ __device__ __forceinline__ void wave_ifft1024(float2 (&x)[16], int lane, float2*
 // of one U block in lockstep (same barriers), each on its own slice image; the tables are shared.
 // The pair's U rows fill 16 of each 32-B sector from one workgroup instead of 8 (the round-3
 // asm_cols_pair experiment: U writes exact), at one 16-wave workgroup per CU.
-template <int NC>
+// A barrier over the 8 waves of one half of the paired workgroup (HB variant, opt-in THZ_K2_4S=3):
+// an LDS counter per half, each wave adds 1 and spins (s_sleep) until it reaches 8 x the calls
+// so far.  The waves of a workgroup are all resident, so it always completes; the spin is still
+// bounded (4096 sleeps) so that a protocol error costs time, never a hang.
+__device__ __forceinline__ void half_barrier(int* ctr, int target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int it = 0; it < 4096; ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+template <int NC, bool HB = false>
 __device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                  const AsmArgs& a) {
   constexpr int PN = fs::N, TT = fs::T;
@@ -757,6 +771,11 @@ __device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, f
     z_hi = (part + 1) * a.nz / a.kparts;
   }
   int* const mz = reinterpret_cast<int*>(tw8 + fs::TW8) + half * (z_hi - z_lo);
+  // HB: the two halves' barrier counters behind the mz words (zeroed before the forward
+  // transform's first workgroup barrier)
+  int* const hb_ctr = reinterpret_cast<int*>(tw8 + fs::TW8) + NC * a.nz + half;
+  if (HB && threadIdx.x < 2) hb_ctr[(int)threadIdx.x - half] = 0;
+  int hb_n = 0;
   const int ncp = (a.ncols + NC - 1) / NC;
   const int bc = id / ncp, cp = NC * (id - bc * ncp) + half;
   const bool live = cp < a.ncols;  // an odd last column: the partner half runs for the barriers only
@@ -843,7 +862,14 @@ __device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, f
       sincos_hw(tf_mul(z, sq[j]), &sn, &cs);
       x[j] = cmul(sp[j], make_float2(cs, a.adjoint ? -sn : sn));
     }
-    wave_ifft1024(x, lane, lds + w * fs::SL, tinv, t64, [] { __syncthreads(); });  // A: the previous z's radix-8 reads are done
+    // A: the previous z's radix-8 reads of this half's slices are done (HB: this half's waves only;
+    // the other half runs on, and B below keeps the two columns within one plane)
+    if constexpr (HB) {
+      hb_n += 8;
+      wave_ifft1024(x, lane, lds + w * fs::SL, tinv, t64, [&] { half_barrier(hb_ctr, hb_n); });
+    } else {
+      wave_ifft1024(x, lane, lds + w * fs::SL, tinv, t64, [] { __syncthreads(); });
+    }
     wf::wave_sync();
 #pragma unroll
     for (int h = 0; h < 16; ++h) lds[w * fs::SL + lane + 64 * h] = x[h];
@@ -886,6 +912,11 @@ asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, As
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
 asm_cols_4s_pair(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_4s_body<2>(T, U, ph, a);
+}
+
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+asm_cols_4s_pair_hb(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_4s_body<2, true>(T, U, ph, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1832,6 +1863,10 @@ static int ensure_lds_attr() {
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)fs::lds_bytes(THZ_MAX_Z, 2));
     if (e6 != hipSuccess) err = e6;
+    const hipError_t e7 = hipFuncSetAttribute((const void*)asm_cols_4s_pair_hb,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)fs::lds_bytes(THZ_MAX_Z, 2) + 8);
+    if (e7 != hipSuccess) err = e7;
     const hipError_t e5 = hipFuncSetAttribute((const void*)asm_rows_inv_4s,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3_4s_lds_bytes());
     if (e5 != hipSuccess) err = e5;
@@ -1870,7 +1905,7 @@ static bool k2_pair(int Ph) {
 static int k2_4s(int Ph, const AsmArgs& a) {
   static const int mode = [] {
     const char* e = getenv("THZ_K2_4S");
-    return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : 0;
+    return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : e && e[0] == '3' ? 3 : 0;
   }();
   return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
 }
@@ -2100,12 +2135,17 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
-      } else if (const int nc4 = k2_4s(g.Ph, a)) {
+      } else if (const int m4 = k2_4s(g.Ph, a)) {
         // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
-        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z), nc4);
-        const void* kern = nc4 == 2 ? (const void*)asm_cols_4s_pair : (const void*)asm_cols_4s;
+        const int nc4 = m4 >= 2 ? 2 : 1;
+        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z), nc4) + (m4 == 3 ? 8 : 0);
+        const void* kern = m4 == 3   ? (const void*)asm_cols_4s_pair_hb
+                           : m4 == 2 ? (const void*)asm_cols_4s_pair
+                                     : (const void*)asm_cols_4s;
         const int ntask = k2_tasks(g, &a, nc4 * fs::T, lds2, nc4 == 2, kern);
-        if (nc4 == 2)
+        if (m4 == 3)
+          hipLaunchKernelGGL(asm_cols_4s_pair_hb, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
+        else if (m4 == 2)
           hipLaunchKernelGGL(asm_cols_4s_pair, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
         else
           hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
