@@ -751,7 +751,8 @@ __device__ __forceinline__ void half_barrier(int* ctr, int target) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <int NC, bool HB = false>
+// HB: barrier A per half; BEVERY > 1: barrier B too, except on every BEVERY-th plane (shared)
+template <int NC, bool HB = false, int BEVERY = 1>
 __device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                  const AsmArgs& a) {
   constexpr int PN = fs::N, TT = fs::T;
@@ -873,7 +874,18 @@ __device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, f
     wf::wave_sync();
 #pragma unroll
     for (int h = 0; h < 16; ++h) lds[w * fs::SL + lane + 64 * h] = x[h];
-    __syncthreads();  // B: every Z_k1 is in its slice
+    // B: every Z_k1 is in its slice (HB with BEVERY > 1: this half's only, except every
+    // BEVERY-th plane, which keeps the two columns within BEVERY planes)
+    if constexpr (HB && BEVERY > 1) {
+      if ((zz - z_lo) % BEVERY == BEVERY - 1) {
+        __syncthreads();
+      } else {
+        hb_n += 8;
+        half_barrier(hb_ctr, hb_n);
+      }
+    } else {
+      __syncthreads();
+    }
     float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -917,6 +929,11 @@ asm_cols_4s_pair(const float2* __restrict__ T, float2* __restrict__ U, FftPlan p
 __global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
 asm_cols_4s_pair_hb(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_4s_body<2, true>(T, U, ph, a);
+}
+
+__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
+asm_cols_4s_pair_hb2(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_4s_body<2, true, 2>(T, U, ph, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1867,6 +1884,10 @@ static int ensure_lds_attr() {
                                               hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)fs::lds_bytes(THZ_MAX_Z, 2) + 8);
     if (e7 != hipSuccess) err = e7;
+    const hipError_t e8 = hipFuncSetAttribute((const void*)asm_cols_4s_pair_hb2,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize,
+                                              (int)fs::lds_bytes(THZ_MAX_Z, 2) + 8);
+    if (e8 != hipSuccess) err = e8;
     const hipError_t e5 = hipFuncSetAttribute((const void*)asm_rows_inv_4s,
                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3_4s_lds_bytes());
     if (e5 != hipSuccess) err = e5;
@@ -1905,7 +1926,7 @@ static bool k2_pair(int Ph) {
 static int k2_4s(int Ph, const AsmArgs& a) {
   static const int mode = [] {
     const char* e = getenv("THZ_K2_4S");
-    return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : e && e[0] == '3' ? 3 : 0;
+    return e && e[0] >= '1' && e[0] <= '4' ? e[0] - '0' : 0;
   }();
   return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
 }
@@ -2138,12 +2159,15 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
       } else if (const int m4 = k2_4s(g.Ph, a)) {
         // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
         const int nc4 = m4 >= 2 ? 2 : 1;
-        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z), nc4) + (m4 == 3 ? 8 : 0);
-        const void* kern = m4 == 3   ? (const void*)asm_cols_4s_pair_hb
+        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z), nc4) + (m4 >= 3 ? 8 : 0);
+        const void* kern = m4 == 4   ? (const void*)asm_cols_4s_pair_hb2
+                           : m4 == 3 ? (const void*)asm_cols_4s_pair_hb
                            : m4 == 2 ? (const void*)asm_cols_4s_pair
                                      : (const void*)asm_cols_4s;
         const int ntask = k2_tasks(g, &a, nc4 * fs::T, lds2, nc4 == 2, kern);
-        if (m4 == 3)
+        if (m4 == 4)
+          hipLaunchKernelGGL(asm_cols_4s_pair_hb2, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
+        else if (m4 == 3)
           hipLaunchKernelGGL(asm_cols_4s_pair_hb, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
         else if (m4 == 2)
           hipLaunchKernelGGL(asm_cols_4s_pair, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);

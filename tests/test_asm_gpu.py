@@ -302,7 +302,7 @@ def test_asm_four_step_k2_matches_three_stage(tmp_path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = []
-    for flag in ("1", "0", "2", "3"):
+    for flag in ("1", "0", "2", "3", "4"):
         path = str(tmp_path / f"k2_{flag}.npy")
         env = dict(os.environ, THZ_K2_4S=flag)
         r = subprocess.run([sys.executable, "-c", _K2_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
@@ -312,6 +312,7 @@ def test_asm_four_step_k2_matches_three_stage(tmp_path):
     assert rel_l2(res[0], res[1]) <= 2e-6
     assert rel_l2(res[2], res[1]) <= 2e-6
     assert rel_l2(res[3], res[1]) <= 2e-6  # THZ_K2_4S=3: the paired kernel with per-half barriers
+    assert rel_l2(res[4], res[1]) <= 2e-6  # THZ_K2_4S=4: and barrier B per half on every other plane
 
 
 def test_asm_middle_crop_kernels_match_the_generic_ones(tmp_path):
