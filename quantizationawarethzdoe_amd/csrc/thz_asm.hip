@@ -344,6 +344,32 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // 2p + 1 in lockstep, each half on its own LDS image, sharing the twiddle tables.  The U sectors
 // (CBU = 4 columns) then have two writers instead of four, and the pair's stores to a sector are
 // issued together.
+// A barrier over the 8 waves of one half of the paired workgroup (the HB paired kernels: asm_cols_4s_pair_hb*, opt-in THZ_K2_4S=3 / 4; asm_cols_pair_hb, THZ_K2_PAIR=2):
+// an LDS counter per half, each wave adds 1 and spins (s_sleep) until it reaches 8 x the calls
+// so far.  The waves of a workgroup are all resident, so it always completes; the spin is still
+// bounded (4096 sleeps) so that a protocol error costs time, never a hang.
+__device__ __forceinline__ void half_barrier(int* ctr, int target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int it = 0; it < 4096; ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// HB: barrier A per half; BEVERY > 1: barrier B too, except on every BEVERY-th plane (shared)
+// the per-half barrier as the FFT exchanges' barrier functor (fft_pow2_io's Bar)
+struct HalfBar {
+  int* ctr;
+  int* n;
+  int waves;
+  __device__ void operator()() const {
+    *n += waves;
+    half_barrier(ctr, *n);
+  }
+};
+
 template <int PN, int NCOL>
 __device__ __forceinline__ int col_tid() {
   if constexpr (NCOL == 2) return (int)threadIdx.x & (Geo<PN>::T - 1);
@@ -353,10 +379,13 @@ __device__ __forceinline__ int col_tid() {
 // MID: the crop is the middle half of the padded column (out_r0 = PN / 4, Hout = PN / 2: padding
 // scale 1 with unpad, cfg2), a compile-time window, so the last stage's outputs outside it and
 // their store tests fold away.
-template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = MID>
+// HB (NCOL = 2): the per-z inverse's exchanges synchronise each half (column) on its own LDS-counter
+// barrier, and one workgroup barrier per plane keeps the two columns together (asm_cols_pair_hb).
+template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = MID, bool HB = false>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
   static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
+  static_assert(!HB || NCOL == 2, "per-half barriers: paired columns only");
   extern __shared__ float2 lds0[];
   // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
   // resident-workgroup count), the last partial round's columns are split into kparts z-ranges
@@ -431,6 +460,10 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     // reference-order tests; the per-element work is then sqrt once per column and one
     // sincos per z.
     int* mz = reinterpret_cast<int*>(lds0 + NCOL * lds_floats2(PN) + tw_lds_count(PN)) + half * THZ_MAX_Z;
+    // HB: the halves' barrier counters behind both mz arrays, zeroed before the barrier below
+    int* const hb_ctr = reinterpret_cast<int*>(lds0 + NCOL * lds_floats2(PN) + tw_lds_count(PN)) + NCOL * THZ_MAX_Z;
+    if (HB && threadIdx.x < 2) hb_ctr[threadIdx.x] = 0;
+    int hb_n = 0;
     const float kl = TWO_PI_F / lam;
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
@@ -531,7 +564,13 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         // streaming stores here ran K2 4.1 -> 13.8 ms)
         if (live && (unsigned)r < (unsigned)(MID ? PN / 2 : a.Hout)) dst[(size_t)r * CBU] = v;
       };
-      fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
+      if constexpr (HB) {
+        fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1,
+                                                          HalfBar{hb_ctr + half, &hb_n, TT / 64});
+        __syncthreads();  // once per plane: the two columns stay together (their U sectors merge)
+      } else {
+        fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
+      }
     }
   } else {
     if constexpr (ZSUM) {
@@ -637,6 +676,12 @@ __global__ void __launch_bounds__(1024) asm_cols_pair(const float2* __restrict__
 }
 
 template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols_pair_hb(const float2* __restrict__ T, float2* __restrict__ U,
+                                                        FftPlan ph, AsmArgs a) {
+  asm_cols_body<PN, false, 2, false, false, true>(T, U, ph, a);
+}
+
+template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols_zsum(const float2* __restrict__ T, float2* __restrict__ U,
                                                      FftPlan ph, AsmArgs a) {
   asm_cols_body<PN, true>(T, U, ph, a);
@@ -737,21 +782,6 @@ __device__ __forceinline__ void wave_ifft1024(float2 (&x)[16], int lane, float2*
 // of one U block in lockstep (same barriers), each on its own slice image; the tables are shared.
 // The pair's U rows fill 16 of each 32-B sector from one workgroup instead of 8 (the round-3
 // asm_cols_pair experiment: U writes exact), at one 16-wave workgroup per CU.
-// A barrier over the 8 waves of one half of the paired workgroup (HB variant, opt-in THZ_K2_4S=3):
-// an LDS counter per half, each wave adds 1 and spins (s_sleep) until it reaches 8 x the calls
-// so far.  The waves of a workgroup are all resident, so it always completes; the spin is still
-// bounded (4096 sleeps) so that a protocol error costs time, never a hang.
-__device__ __forceinline__ void half_barrier(int* ctr, int target) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (int it = 0; it < 4096; ++it) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// HB: barrier A per half; BEVERY > 1: barrier B too, except on every BEVERY-th plane (shared)
 template <int NC, bool HB = false, int BEVERY = 1>
 __device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                  const AsmArgs& a) {
@@ -1873,6 +1903,9 @@ static int ensure_lds_attr() {
     const hipError_t e = hipFuncSetAttribute((const void*)asm_cols_pair<8192>,
                                              hipFuncAttributeMaxDynamicSharedMemorySize, mxp);
     if (e != hipSuccess) err = e;
+    const hipError_t eh = hipFuncSetAttribute((const void*)asm_cols_pair_hb<8192>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, mxp + 8);
+    if (eh != hipSuccess) err = eh;
     const hipError_t e4 = hipFuncSetAttribute((const void*)asm_cols_4s, hipFuncAttributeMaxDynamicSharedMemorySize,
                                               (int)fs::lds_bytes(THZ_MAX_Z));
     if (e4 != hipSuccess) err = e4;
@@ -1913,12 +1946,14 @@ static int mx_kind(int n) { return is_mx(n) ? n : 0; }
 // launch against 14.47 GB for the one-column kernel), but one 16-wave workgroup per CU stalls at
 // every barrier where two 8-wave workgroups overlap theirs: 4.39 ms against 4.16 ms.  The pass is
 // issue-bound, not write-bound, so the one-column kernel stays the default.
-static bool k2_pair(int Ph) {
-  static const bool on = [] {
+// THZ_K2_PAIR=2: asm_cols_pair_hb, the same kernel with per-half LDS-counter barriers in the
+// per-plane inverse and one workgroup barrier per plane.  Returns 0, 1 or 2.
+static int k2_pair(int Ph) {
+  static const int mode = [] {
     const char* e = getenv("THZ_K2_PAIR");
-    return e && e[0] == '1';
+    return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : 0;
   }();
-  return on && Ph == 8192;
+  return Ph == 8192 ? mode : 0;
 }
 // Four-step K2 (asm_cols_4s) at Ph = 8192 for the analytic transfer function (ASM forward and
 // adjoint of one z-chunk); THZ_K2_4S=0 selects the three-stage asm_cols, THZ_K2_4S=2 the paired
@@ -2173,10 +2208,14 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
           hipLaunchKernelGGL(asm_cols_4s_pair, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
         else
           hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
-      } else if (k2_pair(g.Ph)) {
-        const size_t lds2 = k2_pair_lds(g.Ph);
-        const int ntask = k2_tasks(g, &a, 2 * th, lds2, true);
-        hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
+      } else if (const int pm = k2_pair(g.Ph)) {
+        const size_t lds2 = k2_pair_lds(g.Ph) + (pm == 2 ? 8 : 0);
+        const int ntask = k2_tasks(g, &a, 2 * th, lds2, true,
+                                   pm == 2 ? (const void*)asm_cols_pair_hb<8192> : (const void*)asm_cols_pair<8192>);
+        if (pm == 2)
+          hipLaunchKernelGGL(asm_cols_pair_hb<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
+        else
+          hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_range(g.Ph, a)) {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_range<8192>);

@@ -448,9 +448,15 @@ __device__ __forceinline__ int stage_order(int tid) {
     return tid;
 }
 
+// the workgroup barrier of the exchanges (a caller may pass a narrower one, e.g. over one half of
+// a paired-column workgroup whose halves own separate images)
+struct SyncAll {
+  __device__ void operator()() const { __syncthreads(); }
+};
+
 template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, int LIN = 1, int LOUT = L, class Tw,
-          class Ld, class Sv>
-__device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
+          class Ld, class Sv, class Bar = SyncAll>
+__device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv, Bar bar = Bar{}) {
   constexpr int NB = N / R;
   constexpr int MB = NB / T;  // butterflies per thread (exact)
   static_assert(MB * T == NB, "pow2 plan must tile exactly");
@@ -486,7 +492,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     dftR<R, INV>(v[m]);
   }
   if constexpr (OUT_LDS) {
-    __syncthreads();
+    bar();
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
       const int i = bo + m * T;
@@ -496,7 +502,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
 #pragma unroll
       for (int r = 0; r < R; ++r) dst[c64_lay<LOUT>(j0 + r * L) - c64_lay<LOUT>(j0)] = v[m][r];
     }
-    __syncthreads();
+    bar();
   } else {
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
@@ -683,8 +689,8 @@ struct NoIO {
 // Stages S .. NST-1 of a power-of-two transform.  Stage 0 reads through ld unless
 // FIRST_LDS; the final stage writes through sv unless LAST_LDS.
 template <bool INV, int N, int T, int MODE, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1,
-          class Tw, class Ld, class Sv>
-__device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
+          class Tw, class Ld, class Sv, class Bar = SyncAll>
+__device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv, Bar bar = Bar{}) {
   using P = Pow2Sched<N>;
   constexpr int NS = P::nst(MODE);
   if constexpr (S < NS) {
@@ -705,8 +711,8 @@ __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, 
       for (int s = 0; s < 16; ++s) x[s] = src[c64_lay<LIN>(2 * s * LP) - c64_lay<LIN>(0)];
       stage_r32_pair_last<INV, N>(tw, tid, x, sv);
     } else {
-      stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv);
-      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
+      stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv, bar);
+      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv, bar);
     }
   }
 }

@@ -236,20 +236,21 @@ def test_asm_paired_column_kernel_bit_identical():
     """The opt-in paired-column K2 (THZ_K2_PAIR=1, asm_cols_pair<8192>: two band columns per
     workgroup, the odd last column's partner half computing without storing, the z-range split of
     the last dispatch round) gives bit-identical planes to the default one-column kernel on the
-    cfg2 geometry (same arithmetic per column; 6 planes, sha256 of the output)."""
+    cfg2 geometry (same arithmetic per column; 6 planes, sha256 of the output); so does its
+    per-half-barrier form (THZ_K2_PAIR=2, asm_cols_pair_hb)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     code = _PAIR_SCRIPT.format(root=root)
     digests = []
-    for flag in ("1", "0"):
+    for flag in ("1", "0", "2"):
         env = dict(os.environ, THZ_K2_PAIR=flag, THZ_K2_4S="0")
         r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True,
                            timeout=180)
         assert r.returncode == 0, r.stderr[-2000:]
         digests.append(r.stdout.strip().splitlines()[-1])
-    assert digests[0] == digests[1]
+    assert digests[0] == digests[1] == digests[2]
 
 
 _K2_SCRIPT = r"""
