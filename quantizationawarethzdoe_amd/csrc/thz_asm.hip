@@ -1110,7 +1110,9 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
 // per-column sqrt and the bisected |m_x| bound, cropped rows stored from the last stage -- with
 // the runtime plan's numerics at the output (1 / (Ph Pw) is not a power of two here, so the
 // scale is applied to each output element as asm_cols<0> does).
-template <class MP, bool ZSUM>
+// MID: the 300-point layers' windows ([N/3, 2N/3) in and out: padding 2 with unpad, cfg4 / cfg5)
+// as compile-time constants (asm_cols_mx_mid, opt-in THZ_MX_MID=1)
+template <class MP, bool ZSUM, bool MID = false>
 __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                  AsmArgs a) {
   constexpr int PN = MP::N, RL = MP::RL, NBL = PN / RL, MBL = (NBL + MX_T - 1) / MX_T;
@@ -1129,9 +1131,10 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
   const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
   int tid = threadIdx.x;
   float2 sp[MBL][RL];
+  if constexpr (MID) __builtin_assume(tid >= 0 && tid < MX_T);
   auto ld0 = [&](int, int, int idx) {
-    const int s = idx - a.in_r0;
-    return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
+    const int s = idx - (MID ? PN / 3 : a.in_r0);
+    return (s >= 0 && s < (MID ? PN / 3 : a.Hin)) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
   };
   auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
   const auto twr = MP::template twiddles<MX_T>(ph.tw, tid);
@@ -1208,6 +1211,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
     const int M = mzc[zz];
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
+    if constexpr (MID) __builtin_assume(tz >= 0 && tz < MX_T);
     auto ld1 = [&](int m, int r, int idx) {
       const int mx = freq_index(idx, PN);
       if (mx > M || -mx > M) return make_float2(0.f, 0.f);
@@ -1217,8 +1221,8 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
     };
     float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
     auto sv1 = [&](int, int, int j, float2 v) {
-      const int r = j - a.out_r0;
-      if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+      const int r = j - (MID ? PN / 3 : a.out_r0);
+      if ((unsigned)r < (unsigned)(MID ? PN / 3 : a.Hout)) dst[(size_t)r * CBU] = cscale(v, a.scale);
     };
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
   }
@@ -1228,6 +1232,12 @@ template <class MP>
 __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx(
     const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_mx_body<MP, false>(T, U, ph, a);
+}
+
+template <class MP>
+__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_mid(
+    const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
+  asm_cols_mx_body<MP, false, true>(T, U, ph, a);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1982,6 +1992,15 @@ static bool k2_range(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum;
 }
+// the 300-point column pass with its windows as constants (opt-in THZ_MX_MID=1, A/B)
+static bool mx_mid(const AsmArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_MX_MID");
+    return e && e[0] == '1';
+  }();
+  return on && !a.tft && a.in_r0 == Mx300::N / 3 && a.Hin == Mx300::N / 3 && a.out_r0 == Mx300::N / 3 &&
+         a.Hout == Mx300::N / 3;
+}
 // K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid, the default: 4.00 vs 4.13 ms on cfg2;
 // THZ_K3_MID=0 selects asm_rows_inv<8192>)
 static bool k3_mid(int Pw, const AsmArgs& a) {
@@ -2190,7 +2209,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
       } else if (mx_kind(g.Ph) == Mx300::N) {
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
-        hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+        if (mx_mid(a))
+          hipLaunchKernelGGL(asm_cols_mx_mid<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+        else
+          hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
       } else if (const int m4 = k2_4s(g.Ph, a)) {
         // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
         const int nc4 = m4 >= 2 ? 2 : 1;
