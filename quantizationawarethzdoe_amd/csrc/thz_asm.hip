@@ -1111,7 +1111,7 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
 // the runtime plan's numerics at the output (1 / (Ph Pw) is not a power of two here, so the
 // scale is applied to each output element as asm_cols<0> does).
 // MID: the 300-point layers' windows ([N/3, 2N/3) in and out: padding 2 with unpad, cfg4 / cfg5)
-// as compile-time constants (asm_cols_mx_mid, opt-in THZ_MX_MID=1)
+// as compile-time constants (asm_cols_mx_mid, the default for that geometry)
 template <class MP, bool ZSUM, bool MID = false>
 __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                  AsmArgs a) {
@@ -1992,11 +1992,12 @@ static bool k2_range(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum;
 }
-// the 300-point column pass with its windows as constants (opt-in THZ_MX_MID=1, A/B)
+// the 300-point column pass with its windows as constants (asm_cols_mx_mid, the default: 80.8 vs
+// 83.3 us per launch, cfg5 chained 1.097 vs 1.133 ms; THZ_MX_MID=0 selects asm_cols_mx)
 static bool mx_mid(const AsmArgs& a) {
   static const bool on = [] {
     const char* e = getenv("THZ_MX_MID");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on && !a.tft && a.in_r0 == Mx300::N / 3 && a.Hin == Mx300::N / 3 && a.out_r0 == Mx300::N / 3 &&
          a.Hout == Mx300::N / 3;
