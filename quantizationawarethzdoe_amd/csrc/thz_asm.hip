@@ -274,9 +274,11 @@ struct RowSrc {
 };
 
 
-template <int PN>
+// MID (PN = 300 only): the input window [N/3, 2N/3) of the layers' geometry as constants
+template <int PN, bool MID = false>
 __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* __restrict__ in, float2* __restrict__ T,
                                                     FftPlan pw, AsmArgs a) {
+  static_assert(!MID || is_mx(PN), "window constants: the 300-point pass");
   extern __shared__ float2 lds[];
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nrows = gridDim.x - a.tab_blocks;
@@ -310,10 +312,11 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
     };
     fft_pow2_run<false, PN, TT, FFT_ROWS>(lds, twl, tid, ld, sv, tw_hook);
   } else if constexpr (is_mx(PN)) {
+    if constexpr (MID) __builtin_assume(tid >= 0 && tid < MX_T);
     const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
     auto ld = [&](int, int, int idx) {
-      const int s = idx - a.in_c0;
-      return (s >= 0 && s < a.Win) ? fetch(s) : make_float2(0.f, 0.f);
+      const int s = idx - (MID ? PN / 3 : a.in_c0);
+      return (s >= 0 && s < (MID ? PN / 3 : a.Win)) ? fetch(s) : make_float2(0.f, 0.f);
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int c = band_col(j, PN, a.J, a.ncols);
@@ -1569,8 +1572,9 @@ __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WP
 // ---------------------------------------------------------------------------------------------
 // LOSS: the stored row also feeds the |E|^2 -> normalize -> MSE sums of its batch item
 // (LossAcc; Z == 1 so plane == bc), stored per workgroup in slot (c, r) of b by loss_store_part.
-// MID: the crop is the middle half of the padded row (out_c0 = PN / 4, Wout = PN / 2: padding scale
-// 1 with unpad, cfg2), a compile-time window (as asm_cols_mid)
+// MID: the crop as a compile-time window: the middle half of the padded row for the power-of-two
+// sizes (out_c0 = PN / 4, Wout = PN / 2: padding scale 1 with unpad, cfg2), the middle third for
+// the 300-point layers (out_c0 = Wout = 100: padding 2 with unpad, cfg4 / cfg5)
 template <int PN, bool LOSS, bool MID = false>
 __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw,
                                               const AsmArgs& a) {
@@ -1605,14 +1609,16 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     if constexpr (LOSS) acc.add(v, trow[w], ibase + (unsigned)w);
   };
   if constexpr (is_mx(PN)) {
+    if constexpr (MID) __builtin_assume(tid >= 0 && tid < MX_T);
     const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
     auto ld = [&](int, int, int j) {
       const int c = band_col(j, PN, a.J, a.ncols);
       return c >= 0 ? src[blk_u(c, r, a.Hout)] : make_float2(0.f, 0.f);
     };
+    // (MID: the layers' output window [N/3, 2N/3))
     auto sv = [&](int, int, int j, float2 v) {
-      const int w = j - a.out_c0;
-      if ((unsigned)w < (unsigned)a.Wout) put(w, v);
+      const int w = j - (MID ? PN / 3 : a.out_c0);
+      if ((unsigned)w < (unsigned)(MID ? PN / 3 : a.Wout)) put(w, v);
     };
     Mx300::run<true, MX_T>(lds, twr, tid, ld, sv);
   } else if constexpr (PN > 0) {
@@ -1671,6 +1677,13 @@ template <int PN>
 __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv_mid(const float2* __restrict__ U,
                                                                       float2* __restrict__ out, FftPlan pw, AsmArgs a) {
   rows_inv_body<PN, false, true>(U, out, pw, a);
+}
+
+template <int PN>
+__global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_inv_loss_mid(const float2* __restrict__ U,
+                                                                           float2* __restrict__ out, FftPlan pw,
+                                                                           AsmArgs a) {
+  rows_inv_body<PN, true, true>(U, out, pw, a);
 }
 
 template <int PN>
@@ -1992,13 +2005,20 @@ static bool k2_range(int Ph, const AsmArgs& a) {
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum;
 }
-// the 300-point column pass with its windows as constants (asm_cols_mx_mid, the default: 80.8 vs
-// 83.3 us per launch, cfg5 chained 1.097 vs 1.133 ms; THZ_MX_MID=0 selects asm_cols_mx)
-static bool mx_mid(const AsmArgs& a) {
-  static const bool on = [] {
+// the 300-point passes with the layers' windows as constants: THZ_MX_MID=0 selects the generic
+// kernels (A/B); 2 keeps the constants in the column pass only
+static int mx_mid_mode() {
+  static const int mode = [] {
     const char* e = getenv("THZ_MX_MID");
-    return !(e && e[0] == '0');
+    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
   }();
+  return mode;
+}
+static bool mx_mid_on() { return mx_mid_mode() == 1; }
+// the column pass (asm_cols_mx_mid, the default: 80.8 vs 83.3 us per launch, cfg5 chained 1.097
+// vs 1.133 ms)
+static bool mx_mid(const AsmArgs& a) {
+  const bool on = mx_mid_mode() != 0;
   return on && !a.tft && a.in_r0 == Mx300::N / 3 && a.Hin == Mx300::N / 3 && a.out_r0 == Mx300::N / 3 &&
          a.Hout == Mx300::N / 3;
 }
@@ -2009,7 +2029,12 @@ static bool k3_mid(int Pw, const AsmArgs& a) {
     const char* e = getenv("THZ_K3_MID");
     return !(e && e[0] == '0');
   }();
-  return on && Pw == 8192 && a.out_c0 == Pw / 4 && a.Wout == Pw / 2;
+  return (on && Pw == 8192 && a.out_c0 == Pw / 4 && a.Wout == Pw / 2) ||
+         (mx_mid_on() && Pw == Mx300::N && a.out_c0 == Pw / 3 && a.Wout == Pw / 3);
+}
+// K1 of the 300-point layers with the input window as constants (asm_rows_fwd<300, true>)
+static bool k1_mid(int Pw, const AsmArgs& a) {
+  return mx_mid_on() && Pw == Mx300::N && a.in_c0 == Pw / 3 && a.Win == Pw / 3;
 }
 // Four-step K3 (asm_rows_inv_4s) at Pw = 8192, opt-in THZ_K3_4S=1 (A/B against asm_rows_inv<8192>).
 static bool k3_4s(int Pw) {
@@ -2119,6 +2144,9 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
       if (k1_m3(g.Pw, a)) {
         hipLaunchKernelGGL(asm_rows_fwd_m3, dim3((a.nz * g.BC * g.Hin + 1) / 2), dim3(64), m3_rows_fwd_lds_bytes(), s,
                            (const float2*)in, T, pw, a);
+      } else if (k1_mid(g.Pw, a)) {
+        hipLaunchKernelGGL((asm_rows_fwd<Mx300::N, true>), dim3(a.nz * g.BC * g.Hin), dim3(MX_T), fft_lds_bytes_io(g.Pw),
+                           s, (const float2*)in, T, pw, a);
       } else {
         THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(a.nz * g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in,
                         T, pw, a);
@@ -2182,6 +2210,9 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     if (k1_m3(g.Pw, a)) {
       hipLaunchKernelGGL(asm_rows_fwd_m3, dim3((g.BC * g.Hin + 1) / 2 + a.tab_blocks), dim3(64),
                          m3_rows_fwd_lds_bytes(), s, (const float2*)in, T, pw, a);
+    } else if (k1_mid(g.Pw, a)) {
+      hipLaunchKernelGGL((asm_rows_fwd<Mx300::N, true>), dim3(g.BC * g.Hin + a.tab_blocks), dim3(MX_T),
+                         fft_lds_bytes_io(g.Pw), s, (const float2*)in, T, pw, a);
     } else {
       THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(g.BC * g.Hin + a.tab_blocks), fft_lds_bytes_io(g.Pw), s,
                       (const float2*)in, T, pw, a);
@@ -2263,6 +2294,9 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         if (m3) {
           hipLaunchKernelGGL(asm_rows_inv_m3<true>, g3, dim3(64), m3_lds_bytes(), s, (const float2*)U, (float2*)out,
                              pw, a);
+        } else if (g.Pw == Mx300::N && k3_mid(g.Pw, a)) {
+          hipLaunchKernelGGL(asm_rows_inv_loss_mid<Mx300::N>, dim3(a.nz * g.BC * g.Hout), dim3(MX_T),
+                             fft_lds_bytes_io(g.Pw), s, (const float2*)U, (float2*)out, pw, a);
         } else {
           THZ_ROWS_SWITCH(g.Pw, asm_rows_inv_loss, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s,
                           (const float2*)U, (float2*)out, pw, a);
@@ -2276,8 +2310,12 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         hipLaunchKernelGGL(asm_rows_inv_4s, dim3((a.nz * g.BC * g.Hout + K3_RPW - 1) / K3_RPW), dim3(fs::T),
                            k3_4s_lds_bytes(), s, (const float2*)U, (float2*)out, pw, a);
       } else if (k3_mid(g.Pw, a)) {
-        hipLaunchKernelGGL(asm_rows_inv_mid<8192>, dim3(a.nz * g.BC * g.Hout), dim3(threads_for(8192)),
-                           fft_lds_bytes_io(8192), s, (const float2*)U, (float2*)out, pw, a);
+        if (g.Pw == 8192)
+          hipLaunchKernelGGL(asm_rows_inv_mid<8192>, dim3(a.nz * g.BC * g.Hout), dim3(threads_for(8192)),
+                             fft_lds_bytes_io(8192), s, (const float2*)U, (float2*)out, pw, a);
+        else
+          hipLaunchKernelGGL(asm_rows_inv_mid<Mx300::N>, dim3(a.nz * g.BC * g.Hout), dim3(MX_T),
+                             fft_lds_bytes_io(g.Pw), s, (const float2*)U, (float2*)out, pw, a);
       } else {
         THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(a.nz * g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
                         (float2*)out, pw, a);
