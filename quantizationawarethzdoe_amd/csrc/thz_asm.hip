@@ -350,7 +350,8 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // A barrier over the 8 waves of one half of the paired workgroup (the HB paired kernels: asm_cols_4s_pair_hb*, opt-in THZ_K2_4S=3 / 4; asm_cols_pair_hb, THZ_K2_PAIR=2):
 // an LDS counter per half, each wave adds 1 and spins (s_sleep) until it reaches 8 x the calls
 // so far.  The waves of a workgroup are all resident, so it always completes; the spin is still
-// bounded (4096 sleeps) so that a protocol error costs time, never a hang.
+// bounded (4096 sleeps) so that a protocol error costs time, never a hang (and would show as a
+// parity failure: these kernels are opt-in and covered by the K2 variant tests).
 __device__ __forceinline__ void half_barrier(int* ctr, int target) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
