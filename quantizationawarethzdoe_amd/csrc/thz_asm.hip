@@ -385,7 +385,7 @@ __device__ __forceinline__ int col_tid() {
 // their store tests fold away.
 // HB (NCOL = 2): the per-z inverse's exchanges synchronise each half (column) on its own LDS-counter
 // barrier, and one workgroup barrier per plane keeps the two columns together (asm_cols_pair_hb).
-template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = MID, bool HB = false>
+template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = MID, bool HB = false, int ORD = 0>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
   static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
@@ -573,7 +573,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
                                                           HalfBar{hb_ctr + half, &hb_n, TT / 64});
         __syncthreads();  // once per plane: the two columns stay together (their U sectors merge)
       } else {
-        fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
+        fft_pow2_io<true, PN, TT, FFT_TAIL, false, false, 0, 1, ORD>(lds, twl, tz, ld1, sv1);
       }
     }
   } else {
@@ -665,6 +665,13 @@ template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols_range(const float2* __restrict__ T, float2* __restrict__ U,
                                                       FftPlan ph, AsmArgs a) {
   asm_cols_body<PN, false, 1, false, true>(T, U, ph, a);
+}
+
+// (A/B, opt-in THZ_K2_ORD=1: asm_cols with the last stage's stores in ascending row order)
+template <int PN>
+__global__ void __launch_bounds__(1024) asm_cols_ord(const float2* __restrict__ T, float2* __restrict__ U,
+                                                    FftPlan ph, AsmArgs a) {
+  asm_cols_body<PN, false, 1, false, false, false, 1>(T, U, ph, a);
 }
 
 template <int PN>
@@ -1896,6 +1903,7 @@ static void add_kernels(std::vector<const void*>& ks) {
   if constexpr (PN == 8192) {
     ks.push_back((const void*)asm_cols_mid<PN>);
     ks.push_back((const void*)asm_cols_range<PN>);
+    ks.push_back((const void*)asm_cols_ord<PN>);
     ks.push_back((const void*)asm_rows_inv_mid<PN>);
   }
   ks.push_back((const void*)asm_cols_zsum<PN>);
@@ -1998,6 +2006,13 @@ static bool k2_mid(int Ph, const AsmArgs& a) {
     return e && e[0] == '1';
   }();
   return on && Ph == 8192 && !a.tft && !a.zsum && a.out_r0 == Ph / 4 && a.Hout == Ph / 2;
+}
+static bool k2_ord(int Ph, const AsmArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("THZ_K2_ORD");
+    return e && e[0] == '1';
+  }();
+  return on && Ph == 8192 && !a.tft && !a.zsum;
 }
 static bool k2_range(int Ph, const AsmArgs& a) {
   static const bool on = [] {
@@ -2271,6 +2286,10 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
           hipLaunchKernelGGL(asm_cols_pair_hb<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
         else
           hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
+      } else if (k2_ord(g.Ph, a)) {
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_ord<8192>);
+        hipLaunchKernelGGL(asm_cols_ord<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       } else if (k2_range(g.Ph, a)) {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_range<8192>);

@@ -572,7 +572,9 @@ __device__ __forceinline__ void swap_halves(float& a, float& b) {
   b = __int_as_float(r[1]);
 }
 
-template <bool INV, int N, class Tw, class Sv>
+// ORD = 1: the p-loop starts at p = 4 (for a centred half crop the kept rows then go out in
+// ascending order; an A/B of the store order's effect on the L2's sector merging, asm_cols_ord)
+template <bool INV, int N, int ORD = 0, class Tw, class Sv>
 __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float2 (&x)[16], Sv& sv) {
   constexpr int L = N / 32;
   // exp(-2 pi i q / 32) = (C32C[q], -C32S[q]), q < 16
@@ -618,7 +620,8 @@ __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float
   const float2 wi = twat(tw, i);
   const float2 f = e ? cmul(wi, make_float2(C32C[1], -C32S[1])) : wi;  // w^i w32^e
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
+  for (int pp = 0; pp < 8; ++pp) {
+    const int p = ORD ? (pp + 4) & 7 : pp;
     float2 a = x[2 * p], b = x[2 * p + 1];
     swap_halves(a.x, b.x);
     swap_halves(a.y, b.y);
@@ -688,7 +691,7 @@ struct NoIO {
 
 // Stages S .. NST-1 of a power-of-two transform.  Stage 0 reads through ld unless
 // FIRST_LDS; the final stage writes through sv unless LAST_LDS.
-template <bool INV, int N, int T, int MODE, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1,
+template <bool INV, int N, int T, int MODE, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1, int ORD = 0,
           class Tw, class Ld, class Sv, class Bar = SyncAll>
 __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv, Bar bar = Bar{}) {
   using P = Pow2Sched<N>;
@@ -709,10 +712,10 @@ __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, 
       float2 x[16];
 #pragma unroll
       for (int s = 0; s < 16; ++s) x[s] = src[c64_lay<LIN>(2 * s * LP) - c64_lay<LIN>(0)];
-      stage_r32_pair_last<INV, N>(tw, tid, x, sv);
+      stage_r32_pair_last<INV, N, ORD>(tw, tid, x, sv);
     } else {
       stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv, bar);
-      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv, bar);
+      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R, ORD>(lds, tw, tid, ld, sv, bar);
     }
   }
 }

@@ -339,6 +339,24 @@ def test_asm_middle_crop_kernels_match_the_generic_ones(tmp_path):
     assert rel_l2(res[0], res[1]) <= 2e-6
 
 
+def test_asm_k2_store_order_variant_is_bit_identical(tmp_path):
+    """asm_cols_ord (THZ_K2_ORD=1: the last stage's cropped stores in ascending row order, an A/B of
+    the store order) computes the same butterflies as asm_cols<8192>: bit-identical planes."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for flag in ("1", "0"):
+        path = str(tmp_path / f"ord_{flag}.npy")
+        env = dict(os.environ, THZ_K2_ORD=flag)
+        r = subprocess.run([sys.executable, "-c", _K2_SCRIPT.format(root=root, path=path)], env=env, cwd=root,
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(np.load(path))
+    assert rel_l2(res[0], res[1]) <= 2e-6
+
+
 _M3_SCRIPT = r"""
 import sys, numpy as np, torch
 sys.path.insert(0, {root!r})
