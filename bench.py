@@ -333,6 +333,123 @@ def qat_quality_6000(dev, seed=0, iters=6000):
             "reference_source": "plot_data/example_1/loss_curve_Ours.npy (tests/golden/qat_curves.json)"}
 
 
+def check_qat_multi(dev, which):
+    """Outside the timed region: the reference's own 20-step trace of the dual-plane hologram
+    (``which`` = "dual") or the extended depth of focus ("edof") -- tests/golden/qat_{which}_golden.npz,
+    made by tests/golden/gen_qat_multi.py: its initial weight, every Gumbel / height-noise draw and
+    (edof) every re-drawn plane replayed in order -- through the same system, kernels and AdamW;
+    per-step loss within 1e-3 relative (tests/test_qat_multi_gpu.py)."""
+    import numpy as np
+    from quantizationawarethzdoe_amd import qat
+    with np.load(os.path.join(ROOT, "tests", "golden", f"qat_{which}_golden.npz"), allow_pickle=False) as z:
+        A = {k: z[k] for k in z.files}
+    with open(os.path.join(ROOT, "tests", "golden", "qat_multi_manifest.json")) as fh:
+        q = json.load(fh)[which]
+    if which == "dual":
+        system, target = qat.DualPlaneSystem(device=dev), qat.logo_targets(device=dev)
+    else:
+        system, target = qat.ExtendedDOFSystem(device=dev), qat.edof_target(device=dev)
+        nxt = iter(A["zs"][1:])
+
+        def next_planes():
+            zs = next(nxt, None)
+            if zs is not None:
+                for p, zz in zip(system.props, zs):
+                    p.z = float(zz)
+        system.after_forward = next_planes
+    with torch.no_grad():
+        dict(system.doe.named_parameters())[q["param"]].copy_(torch.from_numpy(A["w0"]))
+    trainer = qat.QATTrainer(system, target, lr=q["lr"], max_itrs=q["steps"], optimizer=q["optimizer"])
+    expo, unif = [], []
+    for st in range(q["steps"]):
+        for i, k in enumerate(q["draws"][st]):
+            (expo if k == "expo" else unif).append(A[f"step{st}__draw{i}"])
+    expo.reverse()
+    unif.reverse()
+    system.doe._gumbel_noise = lambda shape, like: torch.from_numpy(expo.pop()).to(like.device)
+    orig = torch.rand_like
+    torch.rand_like = lambda t, *a, **kw: torch.from_numpy(unif.pop()).to(device=t.device, dtype=t.dtype)
+    try:
+        losses = [float(trainer.step().detach()) for _ in range(q["steps"])]
+    finally:
+        torch.rand_like = orig
+    ref = np.array(q["losses"])
+    rel = np.abs(np.array(losses) - ref) / ref
+    return {"ok": bool(rel.max() <= 1e-3 and not expo and not unif), "tol": 1e-3, "max_rel_loss": float(rel.max()),
+            "steps": q["steps"], "reference": f"tests/golden/qat_{which}_golden.npz (the reference's own fp32 trace)"}
+
+
+def qat_multi_quality_6000(dev, which, seed=0, iters=6000):
+    """Outside the timed region: the notebook's whole "Ours" run of the multi-plane system (6,000
+    iterations, iter_frac = itr / 6000, AdamW) on the graph-replayed trainer, final / minimum /
+    last-100-mean against the reference's curve (plot_data/example_2 or example_3
+    loss_curve_Ours.npy via tests/golden/qat_curves.json); ok: the minimum and the last-100 mean
+    within [0.5x, 2x] (tests/test_qat_quality_gpu.py runs three seeds)."""
+    import numpy as np
+    from quantizationawarethzdoe_amd import qat
+    ex = {"dual": "example_2", "edof": "example_3"}[which]
+    with open(os.path.join(ROOT, "tests", "golden", "qat_curves.json")) as fh:
+        ref = json.load(fh)[ex]["methods"]["Ours"]
+    torch.manual_seed(seed)
+    if which == "dual":
+        system, target, lr = qat.DualPlaneSystem(device=dev), qat.logo_targets(device=dev), 0.01
+    else:
+        system, target, lr = qat.ExtendedDOFSystem(seed=seed, device=dev), qat.edof_target(device=dev), 0.02
+    trainer = qat.QATTrainer(system, target, lr=lr, max_itrs=iters, graph=True, optimizer="adamw")
+    curve, dt = trainer.train(iters, log_every=0)
+    c = curve.double().numpy()
+    st = {"final": float(c[-1]), "min": float(c.min()), "mean_last100": float(c[-100:].mean())}
+    ok = bool(np.all(np.isfinite(c)) and all(0.5 * ref[k] <= st[k] <= 2.0 * ref[k] for k in ("min", "mean_last100")))
+    return {"iterations": iters, "seconds": round(dt, 2), "ok": ok, **{k: float(f"{v:.4g}") for k, v in st.items()},
+            "reference": {k: float(f"{ref[k]:.4g}") for k in ("final", "min", "mean_last100")},
+            "reference_source": f"plot_data/{ex}/loss_curve_Ours.npy (tests/golden/qat_curves.json)"}
+
+
+def bench_qat_multi(dev, rank, world, which, steps=60, dist=None):
+    """cfg4 family, secondary lines: the reference's two multi-plane QAT systems -- the dual-plane
+    hologram (plot_data/example_2: v3 DOE, planes 100 / 150 mm, P = 300) and the extended depth of
+    focus (example_3: rotationally symmetric v3, five planes re-drawn every iteration, P = 500, the
+    runtime mixed-radix plan) -- iterations/s per schedule phase on the graph-replayed trainer: every
+    plane from one pipeline (modulation fused into the shared row pass, one column pass over the
+    planes, the Z-summing adjoint in backward), the planes read from the device step state, the
+    one-bucket gradient all-reduce across ranks.  Then the reference's 20-step trace (check_qat_multi)
+    and one 6,000-iteration run against the published curve."""
+    from quantizationawarethzdoe_amd import qat
+    torch.manual_seed(1234 + rank)
+    if which == "dual":
+        system, target, lr = qat.DualPlaneSystem(device=dev), qat.logo_targets(device=dev), 0.01
+    else:
+        system, target, lr = qat.ExtendedDOFSystem(seed=rank, device=dev), qat.edof_target(device=dev), 0.02
+    trainer = qat.QATTrainer(system, target, lr=lr, max_itrs=6000, graph=True, capture_collective=True,
+                             optimizer="adamw")
+    out = {}
+    for name, frac in (("continuous", 0.1), ("blend", 0.5), ("quantized", 0.9)):
+        for _ in range(5):
+            trainer.step(frac)
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            loss = trainer.step(frac)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        out[name] = {"it_per_s": round(steps / dt, 1), "ms_per_it": round(dt / steps * 1e3, 3),
+                     "loss": round(float(loss.detach()), 6)}
+    desc = {"dual": "dual-plane hologram (example_2: v3 DOE 100^2, planes 100 / 150 mm, ASM P=300)",
+            "edof": "extended depth of focus (example_3: rotationally symmetric v3 DOE 100^2, five planes "
+                    "re-drawn every iteration, ASM P=500)"}[which]
+    return {"workload": f"QAT step of the {desc}: all planes in one pipeline, fused loss over the planes, "
+                        "Z-summing adjoint, AdamW, HIP-graph replay per schedule phase, gradient all-reduce "
+                        "over ranks", "planes": len(system.planes),
+            "graph_collective": bool(trainer.allreduce.capturable and trainer.capture_collective), "phases": out,
+            "output_check": check_qat_multi(dev, which), "quality_6000": qat_multi_quality_6000(dev, which)}
+
+
 def check_donn(dev, chained):
     """Outside the timed region: one cfg5 step at the bench's batch (256) through the same model,
     kernels and loss (eager, the noise injected), vs the REFERENCE's own fp64 loss and weight
@@ -449,25 +566,6 @@ def per_rank_shares(dev, x, lam, sp, world=8):
                     "measurement", "cfg2_8_planes": cfg2,
             "cfg3_4_wavelengths": {k: czt[k] for k in ("ms_per_call", "kernel_avg_ms", "output_check")},
             "cfg5_batch_32": {m: {k: v[k] for k in ("ms_per_step", "output_check")} for m, v in donn["modes"].items()}}
-
-
-def load_traffic():
-    """(HBM bytes per launch of each kernel, where they come from): the committed rocprofv3 PMC
-    summary (scripts/pmc_summary.py: (2 FETCH_SIZE + WRITE_SIZE) x 1 KiB, the gfx950 correction),
-    written by a separate profiling run -- NOT measured in this bench run (PMC counters need their
-    own rocprofv3 passes); ``_meta`` names the profile and the kernel build it was taken on."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
-        return None, None
-    try:
-        with open(path) as fh:
-            d = json.load(fh)
-    except Exception:
-        return None, None
-    meta = d.pop("_meta", None) or {}
-    src = (f"profiles/pmc_traffic.json from rocprofv3 PMC passes ({meta.get('profile', 'profile unnamed')}, "
-           f"{meta.get('date', 'date unrecorded')}); a separate profiling run, not this bench run")
-    return d, src
 
 
 def cpu_model():
@@ -664,7 +762,7 @@ def main():
     ap.add_argument("--cpu-planes", type=int, default=64, help="cpu_baseline sample size (whole 4096^2 planes)")
     ap.add_argument("--cpu-budget", type=float, default=30.0, help="cpu_baseline time budget, seconds")
     ap.add_argument("--headline-only", action="store_true", help="skip the cfg3 / cfg4 / cfg5 secondary measurements")
-    ap.add_argument("--secondary-timeout", type=float, default=300.0,
+    ap.add_argument("--secondary-timeout", type=float, default=420.0,
                     help="seconds the cfg3 / cfg4 / cfg5 secondaries may take before the line is printed without them")
     ap.add_argument("--cpu-only", action="store_true",
                     help="time only the cpu_baseline leg (e.g. --cpu-planes 64 --cpu-budget 1e9 for the whole sweep)")
@@ -737,7 +835,7 @@ def main():
     # z the column pass reads and writes H*Pw, the row-inverse pass reads H*Pw and writes H*W).  The
     # kernels must move less: only the ncols band columns can be non-zero and the column spectrum
     # stays in registers across the z-chunk.  That minimum ("pruned") grades the roofline; the
-    # SURVEY figure is kept under roofline_survey_model, the PMC bytes as roofline.traffic.
+    # SURVEY figure is kept under roofline_survey_model.
     ncols, zc = asm_plan_info(1, 1, N_FIELD, N_FIELD, pad, pad, True, 1, lam, sp, zs, args.z_chunk)
     H = W = N_FIELD
     Pw = 2 * N_FIELD
@@ -745,56 +843,43 @@ def main():
              "asm_rows_inv": 8 * zc * (H * Pw + H * W)}
     pruned = {"asm_rows_fwd": 8 * (H * W + ncols * H), "asm_cols": 8 * (ncols * H + zc * ncols * H),
               "asm_rows_inv": 8 * (zc * ncols * H + zc * H * W)}
-    traffic, traffic_src = load_traffic()
-    traffic = traffic or {}
     stats = {}
     for k, (ms, n) in kern.items():
         if n:
             avg = ms / n
             stats[k] = {"avg_ms": avg, "launches": n, "alg_bytes": model[k], "pruned_bytes": pruned[k],
                         "gbs": model[k] / (avg * 1e-3) / 1e9, "gbs_pruned": pruned[k] / (avg * 1e-3) / 1e9}
-            if traffic.get(k):
-                stats[k]["pmc_bytes"] = traffic[k]
-                stats[k]["gbs_pmc"] = traffic[k] / (avg * 1e-3) / 1e9
-    dom = max(stats, key=lambda k: stats[k]["avg_ms"] * stats[k]["launches"]) if stats else None
     total_alg = sum(pruned[k] * stats[k]["launches"] for k in stats) / args.steps
-    total_pmc = (sum(traffic[k] * stats[k]["launches"] for k in stats) / args.steps
-                 if all(traffic.get(k) for k in stats) else None)
-    roof = roof_model = roof_step = roof_ns = None
-    if dom:
-        # roofline.achieved = the bytes the dominant kernel must move (the band-pruned minimum: only
-        # the ncols spectral columns that can be non-zero, the column spectrum kept in registers)
-        # / its live average launch time; it cannot exceed what the kernel moves, so frac <= 1
-        # whichever kernel dominates.  traffic = the PMC-measured HBM bytes of one launch.
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(stats[dom]["gbs_pruned"], 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(stats[dom]["gbs_pruned"] / HBM_PEAK_GBS, 4),
-                "traffic": traffic.get(dom),
-                "traffic_gbs": round(stats[dom]["gbs_pmc"], 1) if "gbs_pmc" in stats[dom] else None,
-                "traffic_source": traffic_src,
-                "alg_bytes_per_launch": pruned[dom], "avg_launch_ms": round(stats[dom]["avg_ms"], 4),
+    roof = roof_model = roof_step = None
+    # roofline: ONE fixed kernel, K2 (asm_cols: the column FFT + transfer function, the kernel
+    # north_star grades; K2 and K3 take about the same time, so grading "the dominant" one flipped
+    # between them from box to box).  achieved = the bytes K2 must move (the band-pruned minimum:
+    # only the ncols spectral columns that can be non-zero, the column spectrum kept in registers
+    # across the z-chunk) / its live average launch time (HIP events on the launch stream).
+    # traffic = null: PMC counters need rocprofv3 passes of their own, so no HBM byte count is
+    # measured inside this run; the counter bytes per launch of the same kernels are in
+    # profiles/pmc_traffic.json (a separate profiling run, named there).
+    RK = "asm_cols"
+    if RK in stats:
+        k2 = stats[RK]
+        roof = {"bound": "hbm", "kernel": "asm_cols (K2: column FFT + transfer function, north_star's kernel)",
+                "achieved": round(k2["gbs_pruned"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(k2["gbs_pruned"] / HBM_PEAK_GBS, 4), "traffic": None,
+                "traffic_note": "not measured in this run (PMC counters need their own rocprofv3 passes); "
+                                "profiles/pmc_traffic.json holds the counter bytes per launch of a separate run",
+                "alg_bytes_per_launch": pruned[RK], "avg_launch_ms": round(k2["avg_ms"], 4), "target_frac": 0.40,
                 "bytes_model": f"band-pruned minimum per launch ({ncols} of {Pw} spectral columns can be non-zero; "
-                               f"K2 keeps each column spectrum in registers across the z-chunk): K1 8(HW + ncols H), "
-                               f"K2 8(ncols H + zc ncols H), K3 8 zc (ncols H + HW); traffic = PMC (2 FETCH_SIZE + "
-                               f"WRITE_SIZE) bytes per launch (profiles/pmc_traffic.json)"}
-        # the whole step on the same bytes: every kernel's minimum / the measured step time
-        # north_star's graded kernel, whichever pass dominates: the FFT + transfer-function column
-        # pass (K2) on its band-pruned minimum bytes
-        if "asm_cols" in stats:
-            k2 = stats["asm_cols"]
-            roof_ns = {"kernel": "asm_cols (K2: column FFT + transfer function, north_star's kernel)",
-                       "achieved": round(k2["gbs_pruned"], 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                       "frac": round(k2["gbs_pruned"] / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": pruned["asm_cols"],
-                       "avg_launch_ms": round(k2["avg_ms"], 4), "target_frac": 0.40}
+                               f"K2 keeps each column spectrum in registers across the z-chunk): "
+                               f"8 (ncols H + zc ncols H), zc = {zc}"}
         roof_step = {"achieved": round(total_alg / (ms_per_step * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(total_alg / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "bytes_per_step": total_alg}
         # SURVEY §8(d)'s unpruned 3-pass figure, kept for comparison only: it charges K2 a per-z
-        # re-read of the column that K2 does not do, so it can exceed 1 when K2 dominates
-        roof_model = {"kernel": dom, "achieved": round(stats[dom]["gbs"], 1), "peak": HBM_PEAK_GBS,
-                      "unit": "GB/s", "frac": round(stats[dom]["gbs"] / HBM_PEAK_GBS, 4),
-                      "alg_bytes_per_launch": model[dom],
+        # re-read of the column that K2 does not do, so it exceeds 1 for K2
+        roof_model = {"kernel": RK, "achieved": round(k2["gbs"], 1), "peak": HBM_PEAK_GBS,
+                      "unit": "GB/s", "frac": round(k2["gbs"] / HBM_PEAK_GBS, 4),
+                      "alg_bytes_per_launch": model[RK],
                       "bytes_model": "SURVEY §8(d) 3-pass model, z_chunk planes per launch"}
-    write_amp = {k: round(traffic[k] / pruned[k], 3) for k in stats if traffic.get(k)}
     step_model = 8 * (H * W + H * Pw + len(zs) * (3 * H * Pw + H * W))
 
     line = {
@@ -810,16 +895,13 @@ def main():
                    "band_columns": ncols, "z_chunk": zc, "parallelism": f"z-shard x{world}"},
         "hbm_gbs_band_pruned": round(total_alg * args.steps / elapsed / 1e9 * world, 1),
         "hbm_gbs_survey_model": round(step_model * args.steps / elapsed / 1e9 * world, 1),
-        "hbm_gbs_pmc": round(total_pmc * args.steps / elapsed / 1e9 * world, 1) if total_pmc else None,
         "kernels": {k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                     for k, v in stats.items()},
         "roofline": roof,
         # every pass on the same footing (K2 and K3 trade places as the longer kernel box to box)
         "roofline_by_kernel": {k: round(v["gbs_pruned"] / HBM_PEAK_GBS, 4) for k, v in stats.items()},
-        "roofline_north_star": roof_ns,
         "roofline_step": roof_step,
         "roofline_survey_model": roof_model,
-        "write_amplification": write_amp,
         "output_check": {"ok": checks_ok, "planes": checks},
     }
     if not args.headline_only:
@@ -828,7 +910,10 @@ def main():
         # in a collective) is reported as such by a watchdog that prints the line and ends every rank
         secondary = {}
         snapshot = [{}]
-        secs = (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat), ("cfg5_donn", bench_donn))
+        secs = (("cfg3_czt", bench_czt), ("cfg4_qat", bench_qat),
+                ("cfg4_dual_plane", lambda *a, **k: bench_qat_multi(*a, which="dual", **k)),
+                ("cfg4_extended_dof", lambda *a, **k: bench_qat_multi(*a, which="edof", **k)),
+                ("cfg5_donn", bench_donn))
         watchdog = _secondary_watchdog(line, [k for k, _ in secs], rank, args.secondary_timeout, snapshot)
         for key, fn in secs:
             try:

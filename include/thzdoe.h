@@ -51,12 +51,13 @@ typedef void* thz_stream_t; /* hipStream_t */
 
 /* ABI of this header.  Bumped whenever a descriptor struct changes layout (round 2 appended
  * rng / rng_stream to thz_doe_desc and thz_quant_desc; 4 added thz_asm_transfer_function and
- * thz_rs_kernel, which the bindings require): a caller compares thz_abi_version()
+ * thz_rs_kernel, which the bindings require; 5 appended thz_asm_desc.window_mask, 6 thz_asm_desc.z_dev):
+ * a caller compares thz_abi_version()
  * with the THZ_ABI_VERSION it was compiled against before its first call, since a shorter
  * struct from an older header would make the library read past it.  Descriptors are plain C
  * structs: zero-initialise them (memset / `= {0}` / ctypes defaults) so fields a caller does not
  * know about stay 0 (no noise buffer and no device generator means no noise). */
-#define THZ_ABI_VERSION 5
+#define THZ_ABI_VERSION 6
 
 /* Library identity. */
 const char* thz_version(void);
@@ -96,6 +97,13 @@ typedef struct thz_asm_desc {
    * (the DONN / QAT layer geometry); other geometries return THZ_E_UNSUPPORTED (apply
    * thz_aperture separately), as does an adjoint with Z > 1. */
   const struct thz_aperture_desc* window_mask;
+  /* optional (NULL = none, ABI 6): the Z plane distances in DEVICE memory [Z], read by the kernels
+   * in place of z[] -- a captured HIP graph then replays with whatever the caller writes there
+   * before each replay (the extended-depth-of-focus loop re-draws its five planes every iteration,
+   * experiment_extend_depth_of_focus.ipynb cell 22).  The spectral band is then sized for any z
+   * (the evanescent bound |Ky| <= k; the band limit still masks per element), and z[] (host) may be
+   * NULL.  The caller keeps the values fixed between a forward and its adjoint. */
+  const float* z_dev;
 } thz_asm_desc;
 
 /* Workspace: the row-pass spectrum T [BC][ncols][H], one z-chunk of column-pass output

@@ -210,9 +210,10 @@ class ASM_prop(nn.Module):
             print("The critical distance is {} m, the TF will be fine during the sampling !".format(zc))
         self.check_Zc = False
 
-    def _run(self, field: ElectricField, zs, loss_target=None, out_mask=None):
+    def _run(self, field: ElectricField, zs, loss_target=None, out_mask=None, z_dev=None):
         """[Z, B, C, Ho, Wo]; with ``loss_target`` (one z): (out, QAT loss) from the fused pipeline;
-        ``out_mask``: an aperture folded onto the output (propagation.window_mask_fusable geometry)."""
+        ``out_mask``: an aperture folded onto the output (propagation.window_mask_fusable geometry);
+        ``z_dev``: the planes read from device memory (propagation._asm_desc)."""
         pend = field._take_pending()
         data = pend.field if pend is not None else field.data
         B, C, H, W = data.shape
@@ -236,10 +237,11 @@ class ASM_prop(nn.Module):
                                                pend=pend if fuse else None)
             elif pend is not None and pend.out is None:  # the DOE layer's modulation, fused into the row pass
                 out = _prop.asm_propagate_modulated(pend, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl,
-                                                    mask=out_mask)
+                                                    mask=out_mask, z_dev=z_dev)
             else:
                 x = pend.run() if pend is not None else x
-                out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl, mask=out_mask)
+                out = _prop.asm_propagate(x, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl, mask=out_mask,
+                                          z_dev=z_dev)
         except RuntimeError as err:
             print("##################################################")
             print("An error occurred.  If the error was due to insufficient memory, try decreasing the size of the "
@@ -282,9 +284,13 @@ class ASM_prop(nn.Module):
                              device=field.device)
         return Eout._adopt_host(field)
 
-    def propagate_planes(self, field: ElectricField, z_list) -> torch.Tensor:
-        """Additive API: all planes of ``z_list`` in one call -> [Z, B, C, Ho, Wo]."""
+    def propagate_planes(self, field: ElectricField, z_list, z_dev=None) -> torch.Tensor:
+        """Additive API: all planes of ``z_list`` in one call -> [Z, B, C, Ho, Wo].  ``z_dev``
+        (float32 device [Z], Z <= THZ_MAX_Z): the kernels read the planes from it instead, so a
+        captured graph replays with the values written there before each replay."""
         zs = _z_host(z_list)
+        if z_dev is not None:
+            return self._run(field, zs, z_dev=z_dev)
         outs = []
         for k in range(0, len(zs), _prop._lib.THZ_MAX_Z):
             outs.append(self._run(field, zs[k:k + _prop._lib.THZ_MAX_Z]))

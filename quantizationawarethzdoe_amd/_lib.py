@@ -20,7 +20,7 @@ THZ_E_WORKSPACE = 3
 THZ_E_HIP = 4
 THZ_MAX_WAVELENGTHS = 64
 THZ_MAX_Z = 256
-THZ_ABI_VERSION = 5  # include/thzdoe.h: the descriptor layouts below
+THZ_ABI_VERSION = 6  # include/thzdoe.h: the descriptor layouts below
 
 BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 
@@ -60,6 +60,7 @@ class AsmDesc(ctypes.Structure):
         ("dx", ctypes.c_float), ("dy", ctypes.c_float),
         ("wavelengths", ctypes.POINTER(ctypes.c_float)), ("z", ctypes.POINTER(ctypes.c_float)),
         ("window_mask", ctypes.c_void_p),  # const thz_aperture_desc* (ABI 5), NULL = none
+        ("z_dev", ctypes.c_void_p),  # const float* device [Z] (ABI 6), NULL = the host z
     ]
 
 

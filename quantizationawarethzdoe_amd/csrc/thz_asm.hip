@@ -90,9 +90,13 @@ struct AsmArgs {
   // (adjoint input); apm is the mask on that grid
   int ap_side;
   ApertureArgs apm;
+  const float* zdev;  // thz_asm_desc.z_dev: the plane distances in device memory (nullptr: zv)
   float lam[THZ_MAX_WAVELENGTHS];
   float zv[THZ_MAX_Z];
 };
+
+// plane distance i of the call: from device memory when the caller gave z_dev (graph-replayable)
+__device__ __forceinline__ float zval(const AsmArgs& a, int i) { return a.zdev ? a.zdev[i] : a.zv[i]; }
 
 
 // Per-(wavelength, z) scalars of the transfer function, fp32 with the reference's
@@ -343,54 +347,10 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // ---------------------------------------------------------------------------------------------
 // ZSUM: the Z-summing adjoint's column pass (a separate instantiation, so the forward's register
 // allocation is untouched by it).
-// NCOL = 2 (power-of-two PN <= 8192): one workgroup transforms the adjacent band columns 2p and
-// 2p + 1 in lockstep, each half on its own LDS image, sharing the twiddle tables.  The U sectors
-// (CBU = 4 columns) then have two writers instead of four, and the pair's stores to a sector are
-// issued together.
-// A barrier over the 8 waves of one half of the paired workgroup (the HB paired kernels: asm_cols_4s_pair_hb*, opt-in THZ_K2_4S=3 / 4; asm_cols_pair_hb, THZ_K2_PAIR=2):
-// an LDS counter per half, each wave adds 1 and spins (s_sleep) until it reaches 8 x the calls
-// so far.  The waves of a workgroup are all resident, so it always completes; the spin is still
-// bounded (4096 sleeps) so that a protocol error costs time, never a hang (and would show as a
-// parity failure: these kernels are opt-in and covered by the K2 variant tests).
-__device__ __forceinline__ void half_barrier(int* ctr, int target) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  for (int it = 0; it < 4096; ++it) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// HB: barrier A per half; BEVERY > 1: barrier B too, except on every BEVERY-th plane (shared)
-// the per-half barrier as the FFT exchanges' barrier functor (fft_pow2_io's Bar)
-struct HalfBar {
-  int* ctr;
-  int* n;
-  int waves;
-  __device__ void operator()() const {
-    *n += waves;
-    half_barrier(ctr, *n);
-  }
-};
-
-template <int PN, int NCOL>
-__device__ __forceinline__ int col_tid() {
-  if constexpr (NCOL == 2) return (int)threadIdx.x & (Geo<PN>::T - 1);
-  else return (int)threadIdx.x;
-}
-
-// MID: the crop is the middle half of the padded column (out_r0 = PN / 4, Hout = PN / 2: padding
-// scale 1 with unpad, cfg2), a compile-time window, so the last stage's outputs outside it and
-// their store tests fold away.
-// HB (NCOL = 2): the per-z inverse's exchanges synchronise each half (column) on its own LDS-counter
-// barrier, and one workgroup barrier per plane keeps the two columns together (asm_cols_pair_hb).
-template <int PN, bool ZSUM, int NCOL = 1, bool MID = false, bool RANGE = MID, bool HB = false, int ORD = 0>
+template <int PN, bool ZSUM>
 __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                               AsmArgs a) {
-  static_assert(NCOL == 1 || (PN > 0 && !ZSUM), "paired columns: forward power-of-two pass only");
-  static_assert(!HB || NCOL == 2, "per-half barriers: paired columns only");
-  extern __shared__ float2 lds0[];
+  extern __shared__ float2 lds[];
   // Tasks: the first kfull blocks are whole columns (all nz planes; full dispatch rounds of the
   // resident-workgroup count), the last partial round's columns are split into kparts z-ranges
   // so that round is short instead of a whole column pass on a few CUs.
@@ -403,13 +363,8 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     z_lo = part * a.nz / a.kparts;
     z_hi = (part + 1) * a.nz / a.kparts;
   }
-  const int ntask = NCOL == 1 ? a.ncols : (a.ncols + 1) / 2;  // column tasks per (b, c) plane
-  const int bc = id / ntask, half = NCOL == 1 ? 0 : (int)threadIdx.x / (int)(blockDim.x / NCOL);
-  int c = (id - bc * ntask) * NCOL + half;
-  const bool live = c < a.ncols;  // the odd last column's partner half runs without storing
-  if (!live) c = a.ncols - 1;
-  const int nt = blockDim.x / NCOL;
-  float2* const lds = lds0 + (PN > 0 ? half * lds_floats2(PN) : 0);
+  const int bc = id / a.ncols, c = id - bc * a.ncols;
+  const int nt = blockDim.x;
   const int Ph = a.Ph;
   const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
   const float lam = a.lam[bc % a.C];
@@ -417,7 +372,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
   // Each phase works from its own opaque copy of threadIdx.x: otherwise the compiler CSEs /
   // hoists the forward and inverse transforms' LDS addresses and twiddle loads across the
   // whole kernel and spills (the two transforms share every twiddle address).
-  int tid = col_tid<PN, NCOL>();
+  int tid = threadIdx.x;
   if constexpr (PN > 0) {
     using S = Pow2Sched<PN>;
     constexpr int TT = Geo<PN>::T;
@@ -427,7 +382,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     constexpr int RL = S::radix(S::NST - 1, true);   // radix of the forward's last stage
     constexpr int MBL = PN / RL / TT;                // its butterflies per thread
     float2 sp[MBL][RL];                              // spectrum, element i + r*PN/RL
-    const TwLds twl = load_tw_lds<PN>(lds0 + NCOL * lds_floats2(PN), ph.tw, threadIdx.x, blockDim.x);
+    const TwLds twl = load_tw_lds<PN>(lds + lds_floats2(PN), ph.tw, threadIdx.x, blockDim.x);
     auto ld0 = [&](int, int, int idx) {
       const int s = idx - a.in_r0;
       return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
@@ -444,16 +399,16 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     }
     if (!ZSUM && a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
       const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
-      int tz = col_tid<PN, NCOL>();
+      int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
       auto ld1 = [&](int m, int r, int idx) {
         const float2 t = tcol[idx];
         return cmul(sp[m][r], a.adjoint ? make_float2(t.x, -t.y) : t);
       };
-      float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      float2* dst = U + (size_t)bc * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if (live && r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+        if (r >= 0 && r < a.Hout) dst[u_roff(r)] = cscale(v, a.scale);
       };
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
       return;
@@ -463,17 +418,13 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     // exactly |m_x| <= M_z.  One lane per z finds M_z by bisection with the exact
     // reference-order tests; the per-element work is then sqrt once per column and one
     // sincos per z.
-    int* mz = reinterpret_cast<int*>(lds0 + NCOL * lds_floats2(PN) + tw_lds_count(PN)) + half * THZ_MAX_Z;
-    // HB: the halves' barrier counters behind both mz arrays, zeroed before the barrier below
-    int* const hb_ctr = reinterpret_cast<int*>(lds0 + NCOL * lds_floats2(PN) + tw_lds_count(PN)) + NCOL * THZ_MAX_Z;
-    if (HB && threadIdx.x < 2) hb_ctr[threadIdx.x] = 0;
-    int hb_n = 0;
+    int* mz = reinterpret_cast<int*>(lds + lds_floats2(PN) + tw_lds_count(PN));
     const float kl = TWO_PI_F / lam;
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
     // strided over the chunk: a z_chunk may exceed the workgroup (64 threads at P = 1024)
     for (int zz = tid; zz < z_hi - z_lo; zz += nt) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + zz]);
+      const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + z_lo + zz));
       int lo = -1, hi = PN / 2 + 1;
       const int bl = a.bl, P = a.Ph;
       const float dx = a.dx;
@@ -505,7 +456,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
 #pragma unroll
         for (int r = 0; r < RL; ++r) sp[m][r] = make_float2(0.f, 0.f);
       for (int zz = z_lo; zz < z_hi; ++zz) {
-        const float z = a.zv[a.zoff + zz];
+        const float z = zval(a, a.zoff + zz);
         const int M = mz[zz - z_lo];
         const float2* colz = T + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
         int tz = threadIdx.x;
@@ -530,23 +481,19 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
       auto ld1 = [&](int m, int r, int) { return sp[m][r]; };
-      float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      float2* dst = U + (size_t)bc * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
         const int r = j - a.out_r0;
-        if ((unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = a.zacc ? cadd(dst[(size_t)r * CBU], v) : v;
+        if ((unsigned)r < (unsigned)a.Hout) dst[u_roff(r)] = a.zacc ? cadd(dst[u_roff(r)], v) : v;
       };
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
       return;
     }
     for (int zz = z_lo; zz < z_hi; ++zz) {
-      const float z = a.zv[a.zoff + zz];
+      const float z = zval(a, a.zoff + zz);
       const int M = mz[zz - z_lo];
-      int tz = col_tid<PN, NCOL>();
+      int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
-      // RANGE (asm_cols_range, asm_cols_mid): the opaque copy hides the thread index's range;
-      // restated, the band test below folds to one compare per element (idx = tz + TT m + (PN / RL) r
-      // < PN / 2 is then known per (m, r) at compile time), and with MID the crop's stores too
-      if constexpr (RANGE) __builtin_assume(tz >= 0 && tz < TT);
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
       // the first stage's operands r in [4, 12) are the rows PN/4 <= |m_x| < 3 PN/4: when this
@@ -561,20 +508,14 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
         return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
       };
-      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
       auto sv1 = [&](int, int, int j, float2 v) {
-        const int r = j - (MID ? PN / 4 : a.out_r0);
+        const int r = j - a.out_r0;
         // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2;
         // streaming stores here ran K2 4.1 -> 13.8 ms)
-        if (live && (unsigned)r < (unsigned)(MID ? PN / 2 : a.Hout)) dst[(size_t)r * CBU] = v;
+        if ((unsigned)r < (unsigned)a.Hout) dst[u_roff(r)] = v;
       };
-      if constexpr (HB) {
-        fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1,
-                                                          HalfBar{hb_ctr + half, &hb_n, TT / 64});
-        __syncthreads();  // once per plane: the two columns stay together (their U sectors merge)
-      } else {
-        fft_pow2_io<true, PN, TT, FFT_TAIL, false, false, 0, 1, ORD>(lds, twl, tz, ld1, sv1);
-      }
+      fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
     }
   } else {
     if constexpr (ZSUM) {
@@ -583,7 +524,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
 #pragma unroll
       for (int m = 0; m < FFT_MAXV; ++m) acc[m] = make_float2(0.f, 0.f);
       for (int zz = z_lo; zz < z_hi; ++zz) {
-        const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+        const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + zz));
         const float2* colz = T + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
         int tm = threadIdx.x;
         asm volatile("" : "+v"(tm));
@@ -610,10 +551,10 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       }
       __syncthreads();
       fft_lds<true>(lds, ph, tm, nt);
-      float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+      float2* dst = U + (size_t)bc * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
       for (int r = tm; r < a.Hout; r += nt) {
         const float2 v = cscale(lds[padx(a.out_r0 + r)], a.scale);
-        dst[(size_t)r * CBU] = a.zacc ? cadd(dst[(size_t)r * CBU], v) : v;
+        dst[u_roff(r)] = a.zacc ? cadd(dst[u_roff(r)], v) : v;
       }
       return;
     }
@@ -632,7 +573,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     }
     const float2* tcol = a.tft ? a.tft + ((size_t)(bc % a.C) * a.ncols + c) * Ph : nullptr;
     for (int zz = z_lo; zz < z_hi; ++zz) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + zz));
       int tm = threadIdx.x;
       asm volatile("" : "+v"(tm));
       __syncthreads();  // previous z's readers are done with lds
@@ -645,8 +586,8 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       }
       __syncthreads();
       fft_lds<true>(lds, ph, tm, nt);
-      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
-      for (int r = tm; r < a.Hout; r += nt) dst[(size_t)r * CBU] = cscale(lds[padx(a.out_r0 + r)], a.scale);
+      float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
+      for (int r = tm; r < a.Hout; r += nt) dst[u_roff(r)] = cscale(lds[padx(a.out_r0 + r)], a.scale);
     }
   }
 }
@@ -657,408 +598,10 @@ __global__ void __launch_bounds__(1024) asm_cols(const float2* __restrict__ T, f
   asm_cols_body<PN, false>(T, U, ph, a);
 }
 
-// A/B (opt-in THZ_K2_RANGE=1): asm_cols with the thread index's range restated, so the band test
-// folds to one compare per element (1316 -> 1241 VALU per thread per plane) -- but its reordered
-// stores merge worse in the L2 (U writes 1.9x instead of 1.6x) and it measured 4.18-4.19 vs
-// 4.06-4.08 ms on cfg2 (profiles/r04_experiments.txt)
-template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols_range(const float2* __restrict__ T, float2* __restrict__ U,
-                                                      FftPlan ph, AsmArgs a) {
-  asm_cols_body<PN, false, 1, false, true>(T, U, ph, a);
-}
-
-// (A/B, opt-in THZ_K2_ORD=1: asm_cols with the last stage's stores in ascending row order)
-template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols_ord(const float2* __restrict__ T, float2* __restrict__ U,
-                                                    FftPlan ph, AsmArgs a) {
-  asm_cols_body<PN, false, 1, false, false, false, 1>(T, U, ph, a);
-}
-
-template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols_mid(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
-                                                    AsmArgs a) {
-  asm_cols_body<PN, false, 1, true>(T, U, ph, a);
-}
-
-template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols_pair(const float2* __restrict__ T, float2* __restrict__ U,
-                                                     FftPlan ph, AsmArgs a) {
-  asm_cols_body<PN, false, 2>(T, U, ph, a);
-}
-
-template <int PN>
-__global__ void __launch_bounds__(1024) asm_cols_pair_hb(const float2* __restrict__ T, float2* __restrict__ U,
-                                                        FftPlan ph, AsmArgs a) {
-  asm_cols_body<PN, false, 2, false, false, true>(T, U, ph, a);
-}
-
 template <int PN>
 __global__ void __launch_bounds__(1024) asm_cols_zsum(const float2* __restrict__ T, float2* __restrict__ U,
                                                      FftPlan ph, AsmArgs a) {
   asm_cols_body<PN, true>(T, U, ph, a);
-}
-
-// ---------------------------------------------------------------------------------------------
-// K2 at Ph = 8192 as a four-step transform (the cfg2 column pass).  The per-z inverse
-//   y[1024 n1 + n2] = sum_k1 w8^(n1 k1) w8192^(n2 k1) Z_k1[n2],  Z_k1 = IDFT_1024(X[k1 + 8 k2])
-// runs the eight 1024-point transforms Z_k1 one per wave, with no workgroup barrier inside them,
-// and the radix-8 step across the waves after ONE workgroup exchange; the asm_cols kernel runs
-// three radix-16/32 stages behind two workgroup exchanges (four barriers per z).  Per z:
-//   1. x[j] = X[k1 + 8 (lane + 64 j)] H_z (spectrum and sqrt(k^2 - K^2) in registers, as asm_cols)
-//   2. radix 16 over j (k2 = lane + 64 j: in-lane), twiddle w1024^(lane c)
-//   3. 64-point transform over the lane index a = e + 16 f: v_permlane32/16_swap trade lane bits
-//      5, 4 (f) for register bits 0, 1; radix 4 over f in registers, twiddle w64^(g e); one
-//      wave-private LDS exchange (this wave's slice); radix 16 over e.  Lane l then holds
-//      Z_k1[l + 64 h], h < 16.
-//   4. Z_k1 to the slice, barrier, and each thread runs the radix 8 over k1 for n2 = lane +
-//      64 (2 wave + s), s < 2, storing rows 1024 n1 + n2 of the crop: consecutive lanes write
-//      consecutive rows (the U layout and K3 are unchanged).
-// Two barriers per z: before the slice exchange (the previous z's radix-8 reads are done) and
-// after the Z_k1 writes.  The index maps are checked by a numpy model of this data flow and by
-// the cfg2 parity tests.  Props/ASM_Prop.py:314-378 (the per-z ift2 over the padded column).
-namespace fs {
-constexpr int N = 8192, T = 512;
-// float2 per wave slice: the exchange image (g, c) x e padded to 17 (1088), +4 so that the eight
-// slices' same positions fall on distinct banks (K3's output transpose reads all eight in one access)
-constexpr int SL = 64 * 17 + 4;
-constexpr int IMG = 8 * SL;  // >= lds_floats2(8192) (the forward transform's image)
-constexpr int TINV = 15 * 64;  // w1024^(lane c), [c - 1][lane]
-constexpr int T64 = 3 * 16;    // w64^(g e), [g - 1][e]
-constexpr int TW8 = 64 + 16;   // w8192^n2 = w8192^(n2 & 63) w128^(n2 >> 6), n2 < 1024
-static_assert(IMG >= 8 * SL && IMG >= lds_floats2(N), "slice region");
-__host__ __device__ constexpr size_t lds_bytes(int nz, int nc = 1) {
-  return (size_t)(nc * IMG + TINV + T64 + TW8) * sizeof(float2) + 4 * nc * nz;
-}
-static_assert(lds_bytes(THZ_MAX_Z, 2) + 8 <= 160 * 1024, "paired four-step K2 LDS (+ the HB counters)");
-}  // namespace fs
-
-__device__ __forceinline__ void swap_rows16(float& a, float& b) {
-  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(b), false, false);
-  a = __int_as_float(r[0]);
-  b = __int_as_float(r[1]);
-}
-
-// The 1024-point inverse transform of one wave (the four-step K2 / K3): on entry x[j] holds input
-// k2 = lane + 64 j, on exit x[h] holds output lane + 64 h.  Radix 16 over j in registers, twiddle
-// w1024^(lane c); the 64-point transform over the lane index a = e + 16 f: v_permlane32/16_swap
-// trade lane bits 5, 4 (f) for register bits 0, 1 (c0, c1), radix 4 over f, twiddle w64^(g e),
-// one exchange through this wave's own LDS slice (no workgroup barrier), radix 16 over e.
-// `before` runs just before the slice's first write (the caller's barrier, if other waves may
-// still read the slice).
-template <class Before>
-__device__ __forceinline__ void wave_ifft1024(float2 (&x)[16], int lane, float2* slice, const float2* tinv,
-                                              const float2* t64, Before before) {
-  dft16<true>(x);
-#pragma unroll
-  for (int q = 1; q < 16; ++q) x[q] = cmulc(x[q], tinv[(q - 1) * 64 + lane]);
-  // lane bit 5 <-> register bit 0, lane bit 4 <-> register bit 1: lane e + 16 c1 + 32 c0,
-  // register f1 + 2 f0 + 4 u (u = c >> 2)
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    swap_halves(x[2 * p].x, x[2 * p + 1].x);
-    swap_halves(x[2 * p].y, x[2 * p + 1].y);
-  }
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    if (q & 2) continue;
-    swap_rows16(x[q].x, x[q + 2].x);
-    swap_rows16(x[q].y, x[q + 2].y);
-  }
-  // radix 4 over f = f0 + 2 f1 (registers 4u + {0, 2, 1, 3}); output g at 4u + {0, 2, 1, 3}
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    float2* v = &x[4 * u];
-    dft4<true>(v[0], v[2], v[1], v[3]);
-    v[2] = cmulc(v[2], t64[lane & 15]);
-    v[1] = cmulc(v[1], t64[16 + (lane & 15)]);
-    v[3] = cmulc(v[3], t64[32 + (lane & 15)]);
-  }
-  before();
-  // exchange image positions: write (g, c, e) at (16 g + c) 17 + e from lane e + 16 c1 + 32 c0,
-  // read e at 17 lane + e
-  const int xw = ((lane >> 5) + 2 * ((lane >> 4) & 1)) * 17 + (lane & 15);
-  const int xr = 17 * lane;
-#pragma unroll
-  for (int rho = 0; rho < 16; ++rho) {
-    const int u = rho >> 2, g = ((rho & 1) << 1) | ((rho >> 1) & 1);
-    slice[xw + (16 * g + 4 * u) * 17] = x[rho];
-  }
-  wf::wave_sync();
-#pragma unroll
-  for (int e = 0; e < 16; ++e) x[e] = slice[xr + e];
-  dft16<true>(x);  // x[h] = output lane + 64 h
-}
-
-// NC = 2 (asm_cols_4s_pair, opt-in THZ_K2_4S=2): two 512-thread halves run columns 2p and 2p + 1
-// of one U block in lockstep (same barriers), each on its own slice image; the tables are shared.
-// The pair's U rows fill 16 of each 32-B sector from one workgroup instead of 8 (the round-3
-// asm_cols_pair experiment: U writes exact), at one 16-wave workgroup per CU.
-template <int NC, bool HB = false, int BEVERY = 1>
-__device__ __forceinline__ void asm_cols_4s_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
-                                                 const AsmArgs& a) {
-  constexpr int PN = fs::N, TT = fs::T;
-  extern __shared__ float2 lds_all[];
-  const int half = NC == 2 ? (int)(threadIdx.x >> 9) : 0;
-  float2* const lds = lds_all + half * fs::IMG;
-  float2* const tinv = lds_all + NC * fs::IMG;
-  float2* const t64 = tinv + fs::TINV;
-  float2* const tw8 = t64 + fs::T64;
-  int id, z_lo = 0, z_hi = a.nz;
-  if ((int)blockIdx.x < a.kfull) {
-    id = xcd_chunk(blockIdx.x, a.kfull);
-  } else {
-    const int t = blockIdx.x - a.kfull, part = t % a.kparts;
-    id = a.kfull + t / a.kparts;
-    z_lo = part * a.nz / a.kparts;
-    z_hi = (part + 1) * a.nz / a.kparts;
-  }
-  int* const mz = reinterpret_cast<int*>(tw8 + fs::TW8) + half * (z_hi - z_lo);
-  // HB: the two halves' barrier counters behind the mz words (zeroed before the forward
-  // transform's first workgroup barrier)
-  int* const hb_ctr = reinterpret_cast<int*>(tw8 + fs::TW8) + NC * a.nz + half;
-  if (HB && threadIdx.x < 2) hb_ctr[(int)threadIdx.x - half] = 0;
-  int hb_n = 0;
-  const int ncp = (a.ncols + NC - 1) / NC;
-  const int bc = id / ncp, cp = NC * (id - bc * ncp) + half;
-  const bool live = cp < a.ncols;  // an odd last column: the partner half runs for the barriers only
-  const int c = live ? cp : a.ncols - 1;
-  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
-  const float lam = a.lam[bc % a.C];
-  const float Ky = kfreq(c - a.J, a.Pw, a.dy);
-  const int tid = threadIdx.x & (TT - 1), lane = tid & 63, w = tid >> 6;
-  const float2* __restrict__ tw = ph.tw;  // exp(-2 pi i t / 8192)
-  if (half == 0) {
-    for (int i = tid; i < fs::TINV; i += TT) tinv[i] = tw[8 * (i & 63) * ((i >> 6) + 1)];
-    if (tid < fs::T64) t64[tid] = tw[128 * ((tid >> 4) + 1) * (tid & 15)];
-    if (tid < fs::TW8) tw8[tid] = tw[tid < 64 ? tid : 64 * (tid - 64)];
-  }
-  // kept rows |m_x| <= M_z per z (bisection with the reference-order tests, as asm_cols)
-  {
-    for (int zz = tid; zz < z_hi - z_lo; zz += TT) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + z_lo + zz]);
-      int lo = -1, hi = PN / 2 + 1;
-      if (tf_pass(a.bl, a.Ph, a.dx, s, Ky, 0)) {
-        lo = 0;
-        while (hi - lo > 1) {
-          const int mid = (lo + hi) >> 1;
-          if (tf_pass(a.bl, a.Ph, a.dx, s, Ky, mid)) lo = mid;
-          else hi = mid;
-        }
-      }
-      mz[zz] = lo;
-    }
-  }
-  // forward transform of the zero-padded column (once): thread tid holds X[tid + 512 r]
-  float2 sp[16];
-  {
-    int tf = tid;
-    asm volatile("" : "+v"(tf));
-    auto ld0 = [&](int, int, int idx) {
-      const int s = idx - a.in_r0;
-      return (s >= 0 && s < a.Hin) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
-    };
-    // 1 / (Ph Pw) is a power of two: scaling the spectrum once is exact
-    auto sv0 = [&](int, int r, int, float2 v) { sp[r] = cscale(v, a.scale); };
-    fft_pow2_io<false, PN, TT, 1, false, false>(lds, tw, tf, ld0, sv0);
-  }
-  // redistribute: wave w takes X[w + 8 (lane + 64 j)] (image k + (k >> 5): both access patterns
-  // conflict-free)
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int k = tid + 512 * r;
-    lds[k + (k >> 5)] = sp[r];
-  }
-  __syncthreads();
-  float sq[16];
-  {
-    const float kl = TWO_PI_F / lam;
-    const float kl2 = tf_mul(kl, kl);
-    const float Ky2 = tf_mul(Ky, Ky);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = w + 8 * (lane + 64 * j);
-      sp[j] = lds[k + (k >> 5)];
-      const float Kx = kfreq(freq_index(k, PN), PN, a.dx);
-      sq[j] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
-    }
-  }
-  for (int zz = z_lo; zz < z_hi; ++zz) {
-    const float z = a.zv[a.zoff + zz];
-    const int M = mz[zz - z_lo];
-    // inputs j in [4, 12) are |m_x| >= PN / 4: zero for every lane when M < PN / 4
-    const bool mid0 = __builtin_amdgcn_readfirstlane(M) < PN / 4;
-    // per-iteration opaque copy of the lane index: otherwise the compiler hoists every
-    // lane-dependent address and predicate of the loop body out of it and spills
-    int lane = tid & 63;
-    asm volatile("" : "+v"(lane));
-    const int kb = w + 8 * lane;  // element j is k = kb + 512 j
-    float2 x[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      x[j] = make_float2(0.f, 0.f);
-      if (j >= 4 && j < 12 && mid0) continue;
-      // |m_x| = k (j < 8) or PN - k (j >= 8)
-      if (j < 8 ? kb + 512 * j > M : PN - 512 * j - kb > M) continue;
-      float sn, cs;
-      sincos_hw(tf_mul(z, sq[j]), &sn, &cs);
-      x[j] = cmul(sp[j], make_float2(cs, a.adjoint ? -sn : sn));
-    }
-    // A: the previous z's radix-8 reads of this half's slices are done (HB: this half's waves only;
-    // the other half runs on, and B below keeps the two columns within one plane)
-    if constexpr (HB) {
-      hb_n += 8;
-      wave_ifft1024(x, lane, lds + w * fs::SL, tinv, t64, [&] { half_barrier(hb_ctr, hb_n); });
-    } else {
-      wave_ifft1024(x, lane, lds + w * fs::SL, tinv, t64, [] { __syncthreads(); });
-    }
-    wf::wave_sync();
-#pragma unroll
-    for (int h = 0; h < 16; ++h) lds[w * fs::SL + lane + 64 * h] = x[h];
-    // B: every Z_k1 is in its slice (HB with BEVERY > 1: this half's only, except every
-    // BEVERY-th plane, which keeps the two columns within BEVERY planes)
-    if constexpr (HB && BEVERY > 1) {
-      if ((zz - z_lo) % BEVERY == BEVERY - 1) {
-        __syncthreads();
-      } else {
-        hb_n += 8;
-        half_barrier(hb_ctr, hb_n);
-      }
-    } else {
-      __syncthreads();
-    }
-    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int n2 = lane + 64 * (2 * w + s);
-      float2 v[8];
-#pragma unroll
-      for (int k1 = 0; k1 < 8; ++k1) v[k1] = lds[k1 * fs::SL + n2];
-      // the radix-8 step's twiddles w8192^(n2 k1): w8192^n2 from the two-level table, its powers
-      // formed here (no global loads in the z loop: a load behind the previous z's U stores would
-      // wait for them, vmcnt counts in order)
-      const float2 w1 = cmul(tw8[lane], tw8[64 + 2 * w + s]);
-      const float2 w2 = cmul(w1, w1), w3 = cmul(w1, w2), w4 = cmul(w2, w2);
-      v[1] = cmulc(v[1], w1);
-      v[2] = cmulc(v[2], w2);
-      v[3] = cmulc(v[3], w3);
-      v[4] = cmulc(v[4], w4);
-      v[5] = cmulc(v[5], cmul(w1, w4));
-      v[6] = cmulc(v[6], cmul(w2, w4));
-      v[7] = cmulc(v[7], cmul(w3, w4));
-      dft8<true>(v);
-#pragma unroll
-      for (int n1 = 0; n1 < 8; ++n1) {
-        const int r = 1024 * n1 + n2 - a.out_r0;
-        // (ordinary stores: the 4 column workgroups of a U block fill its 32-B sectors in the L2)
-        if (live && (unsigned)r < (unsigned)a.Hout) dst[(size_t)r * CBU] = v[n1];
-      }
-    }
-  }
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-asm_cols_4s(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
-  asm_cols_4s_body<1>(T, U, ph, a);
-}
-
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
-asm_cols_4s_pair(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
-  asm_cols_4s_body<2>(T, U, ph, a);
-}
-
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
-asm_cols_4s_pair_hb(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
-  asm_cols_4s_body<2, true>(T, U, ph, a);
-}
-
-__global__ void __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(4)))
-asm_cols_4s_pair_hb2(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
-  asm_cols_4s_body<2, true, 2>(T, U, ph, a);
-}
-
-// ---------------------------------------------------------------------------------------------
-// K3 at Pw = 8192 as a four-step transform (opt-in THZ_K3_4S=1, A/B against asm_rows_inv<8192>).
-// With k = 1024 k1 + k2 and n = n1 + 8 n2 the inverse is
-//   y[n1 + 8 n2] = sum_k2 w1024^(n2 k2) [ w8192^(n1 k2) sum_k1 w8^(n1 k1) X[1024 k1 + k2] ],
-// so each thread gathers its two k2 (the band columns of consecutive lanes are consecutive, as in
-// asm_rows_inv) for all k1, runs the radix 8 over k1 in registers, and after ONE workgroup exchange
-// wave n1 runs the 1024-point wave transform over k2 (wave_ifft1024, no workgroup barrier).  A
-// second exchange gives each thread consecutive outputs n for whole-line streaming stores.  Three
-// barriers per row instead of the split-exchange transform's twelve; RPW rows per workgroup share
-// one fill of the twiddle tables.
-constexpr int K3_RPW = 4;
-constexpr size_t k3_4s_lds_bytes() { return (size_t)(fs::IMG + fs::TINV + fs::T64 + fs::TW8) * sizeof(float2); }
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-asm_rows_inv_4s(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw, AsmArgs a) {
-  constexpr int PN = fs::N, TT = fs::T;
-  extern __shared__ float2 lds[];
-  float2* const tinv = lds + fs::IMG;
-  float2* const t64 = tinv + fs::TINV;
-  float2* const tw8 = t64 + fs::T64;
-  const float2* __restrict__ tw = pw.tw;  // exp(-2 pi i t / 8192)
-  const int tid = threadIdx.x, w = tid >> 6;
-  for (int i = tid; i < fs::TINV; i += TT) tinv[i] = tw[8 * (i & 63) * ((i >> 6) + 1)];
-  if (tid < fs::T64) t64[tid] = tw[128 * ((tid >> 4) + 1) * (tid & 15)];
-  if (tid < fs::TW8) tw8[tid] = tw[tid < 64 ? tid : 64 * (tid - 64)];
-  const int rows = a.nz * a.BC * a.Hout;
-  for (int rr = 0; rr < K3_RPW; ++rr) {
-    const int row = (int)blockIdx.x * K3_RPW + rr;
-    if (row >= rows) break;  // uniform over the workgroup
-    const int plane = row / a.Hout, ro = row - plane * a.Hout;
-    const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
-    int lane = tid & 63;
-    asm volatile("" : "+v"(lane));
-    // gather X[1024 k1 + k2] of this thread's k2 = tid + 512 s, then radix 8 over k1 and the
-    // four-step twiddle w8192^(n1 k2)
-    float2 v[2][8];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int k2 = tid + 512 * s;
-#pragma unroll
-      for (int k1 = 0; k1 < 8; ++k1) {
-        const int c = band_col(1024 * k1 + k2, PN, a.J, a.ncols);
-        v[s][k1] = c >= 0 ? src[blk_u(c, ro, a.Hout)] : make_float2(0.f, 0.f);
-      }
-    }
-    if (rr == 0) __syncthreads();  // the tables (their first reads follow)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int k2 = tid + 512 * s;
-      dft8<true>(v[s]);
-      const float2 w1 = cmul(tw8[k2 & 63], tw8[64 + (k2 >> 6)]);
-      const float2 w2 = cmul(w1, w1), w3 = cmul(w1, w2), w4 = cmul(w2, w2);
-      v[s][1] = cmulc(v[s][1], w1);
-      v[s][2] = cmulc(v[s][2], w2);
-      v[s][3] = cmulc(v[s][3], w3);
-      v[s][4] = cmulc(v[s][4], w4);
-      v[s][5] = cmulc(v[s][5], cmul(w1, w4));
-      v[s][6] = cmulc(v[s][6], cmul(w2, w4));
-      v[s][7] = cmulc(v[s][7], cmul(w3, w4));
-    }
-    __syncthreads();  // the previous row's output reads of every slice are done
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int n1 = 0; n1 < 8; ++n1) lds[n1 * fs::SL + tid + 512 * s] = v[s][n1];
-    __syncthreads();
-    float2* const slice = lds + w * fs::SL;  // wave n1 = w
-    float2 x[16];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) x[j] = slice[lane + 64 * j];
-    wave_ifft1024(x, lane, slice, tinv, t64, [] {});  // only this wave reads its slice now
-    wf::wave_sync();
-#pragma unroll
-    for (int h = 0; h < 16; ++h) slice[lane + 64 * h] = x[h];  // y[w + 8 (lane + 64 h)]
-    __syncthreads();
-    float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + ro) * a.Wout;
-    for (int wo = tid; wo < a.Wout; wo += TT) {
-      const int n = a.out_c0 + wo;
-      // written once and never read back here: streaming stores (asm_rows_inv)
-      st_stream(dst + wo, lds[(n & 7) * fs::SL + (n >> 3)]);
-    }
-  }
 }
 
 // Per (wavelength, band column) of a mixed-radix Ph: sqrt(k^2 - Kx^2 - Ky^2) of every row
@@ -1085,7 +628,7 @@ __device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq) {
     // is the number that pass (the kept set is a prefix of |m_x|), instead of one lane's serial
     // bisection
     for (int zz = 0; zz < a.nz; ++zz) {
-      const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+      const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + zz));
       int n = 0;
 #pragma unroll
       for (int m0 = 0; m0 <= PN / 2; m0 += MX_T) {
@@ -1097,7 +640,7 @@ __device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq) {
     return;
   }
   for (int zz = threadIdx.x; zz < a.nz; zz += blockDim.x) {
-    const TfScalars s = tf_scalars(a, lam, a.zv[a.zoff + zz]);
+    const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + zz));
     int lo = -1, hi = PN / 2 + 1;
     if (tf_pass(a.bl, PN, a.dx, s, Ky, 0)) {
       lo = 0;
@@ -1158,10 +701,10 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
       const float2 t = tcol[idx];
       return cmul(sp[m][r], a.adjoint ? make_float2(t.x, -t.y) : t);
     };
-    float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+    float2* dst = U + (size_t)bc * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
     auto sv1 = [&](int, int, int j, float2 v) {
       const int r = j - a.out_r0;
-      if (r >= 0 && r < a.Hout) dst[(size_t)r * CBU] = cscale(v, a.scale);
+      if (r >= 0 && r < a.Hout) dst[u_roff(r)] = cscale(v, a.scale);
     };
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
     return;
@@ -1185,7 +728,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
 #pragma unroll
       for (int r = 0; r < RL; ++r) sp[m][r] = make_float2(0.f, 0.f);
     for (int zz = z_lo; zz < z_hi; ++zz) {
-      const float z = a.zv[a.zoff + zz];
+      const float z = zval(a, a.zoff + zz);
       const int M = mzc[zz];
       const float2* colz = T + ((size_t)zz * a.BC + bc) * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
       int tz = threadIdx.x;
@@ -1206,19 +749,19 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
     auto ld1 = [&](int m, int r, int) { return sp[m][r]; };
-    float2* dst = U + (size_t)bc * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+    float2* dst = U + (size_t)bc * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
     auto sv1 = [&](int, int, int j, float2 v) {
       const int r = j - a.out_r0;
       if ((unsigned)r < (unsigned)a.Hout) {
         const float2 o = cscale(v, a.scale);
-        dst[(size_t)r * CBU] = a.zacc ? cadd(dst[(size_t)r * CBU], o) : o;
+        dst[u_roff(r)] = a.zacc ? cadd(dst[u_roff(r)], o) : o;
       }
     };
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
     return;
   }
   for (int zz = z_lo; zz < z_hi; ++zz) {
-    const float z = a.zv[a.zoff + zz];
+    const float z = zval(a, a.zoff + zz);
     const int M = mzc[zz];
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
@@ -1230,10 +773,10 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
       sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
       return cmul(sp[m][r], make_float2(cs, a.adjoint ? -sn : sn));
     };
-    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout + blk_u(c, 0, a.Hout);
+    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * u_rows(a.Hout) + blk_u(c, 0, a.Hout);
     auto sv1 = [&](int, int, int j, float2 v) {
       const int r = j - (MID ? PN / 3 : a.out_r0);
-      if ((unsigned)r < (unsigned)(MID ? PN / 3 : a.Hout)) dst[(size_t)r * CBU] = cscale(v, a.scale);
+      if ((unsigned)r < (unsigned)(MID ? PN / 3 : a.Hout)) dst[u_roff(r)] = cscale(v, a.scale);
     };
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
   }
@@ -1249,324 +792,6 @@ template <class MP>
 __global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_mid(
     const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_mx_body<MP, false, true>(T, U, ph, a);
-}
-
-// ---------------------------------------------------------------------------------------------
-// K2 at Ph = 300 with the input and output windows both [100, 200) (the cfg4 / cfg5 layers:
-// 100-row fields, padding_scale 2, cropped output): the 300-point column transforms split into
-// three 100-point ones.  With W = exp(-2 pi i / 300) and k = 3 k' + r (r < 3), the forward of the
-// window x'[n'] = x[100 + n'] is
-//   X[3 k' + r] = w3^r DFT_100(x'[n'] W^(r n'))[k'],
-// and the inverse kept rows y[100 + m'] = sum_r w3^-r W^(-r m') IDFT_100(Y[3 k' + r])[m'] -- the
-// w3^(+-r) of one class cancel (Y = X H class by class).  So per column and class r: a pre-twiddle,
-// a 100-point forward, x H_z, a 100-point inverse, a post-twiddle, and a sum over the classes:
-// about 20 % less arithmetic than the padded 300-point pair, and the 100-point transforms run as
-// 10 x 10 (prime-factor radix 10, no inner twiddles) on 60 of the 64 lanes -- two columns per wave,
-// lane = 32 half + 10 r + i -- where the 5 3 4 5 plan keeps 60/100/75/60 butterflies on 64 lanes.
-// Spectrum, sqrt(k^2 - K^2) and bounds as asm_cols_mx (per-column tables); the Z loop keeps the
-// spectrum in registers.  The LDS image of class (half, r) is 100 elements at stride M3_IMS
-// (bank-model search, /tmp-free: both exchanges and the class sum within 1.5x of conflict-free).
-constexpr int M3_L = 100;
-constexpr int M3_IMS = 107;
-constexpr size_t m3_lds_bytes() { return (size_t)6 * M3_IMS * sizeof(float2); }
-
-// 10-point DFT, prime-factor 2 x 5 (no twiddles): input j = (5 j1 + 2 j2) mod 10, output
-// q = (5 q1 + 6 q2) mod 10
-template <bool INV>
-__device__ __forceinline__ void dft10(float2* v) {
-  float2 a[5], b[5];
-#pragma unroll
-  for (int j2 = 0; j2 < 5; ++j2) {
-    a[j2] = v[(2 * j2) % 10];
-    b[j2] = v[(5 + 2 * j2) % 10];
-  }
-  dft5<INV>(a);
-  dft5<INV>(b);
-#pragma unroll
-  for (int q2 = 0; q2 < 5; ++q2) {
-    v[(6 * q2) % 10] = cadd(a[q2], b[q2]);
-    v[(5 + 6 * q2) % 10] = csub(a[q2], b[q2]);
-  }
-}
-
-// ONEZ: one z-plane per launch (the layers' case): the spectrum is consumed in place by the
-// transfer-function product instead of being held across a z loop (20 registers fewer: 8 waves /
-// SIMD without spills; the Z-loop form runs at 5)
-template <bool ONEZ>
-__device__ __forceinline__ void asm_cols_m3_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
-                                                 const AsmArgs& a) {
-  constexpr int PN = 3 * M3_L;
-  extern __shared__ float2 lds[];
-  int id, z_lo = 0, z_hi = a.nz;
-  if ((int)blockIdx.x < a.kfull) {
-    id = xcd_chunk(blockIdx.x, a.kfull);
-  } else {
-    const int t = blockIdx.x - a.kfull, part = t % a.kparts;
-    id = a.kfull + t / a.kparts;
-    z_lo = part * a.nz / a.kparts;
-    z_hi = (part + 1) * a.nz / a.kparts;
-  }
-  const int npair = (a.ncols + 1) / 2;
-  const int bc = id / npair, pr = id - bc * npair;
-  const int lane = threadIdx.x, h = lane >> 5, rem = lane & 31;
-  const bool act = rem < 30;                        // lanes 30, 31 of each half idle
-  const int r = act ? rem / 10 : 0, i = act ? rem - 10 * r : 0;
-  int c = 2 * pr + h;
-  if (c >= a.ncols) c = a.ncols - 1;                // the odd last column's partner half: no stores
-  const float2* __restrict__ tw = ph.tw;           // W^t, t < 300
-  const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
-  float2* img = lds + (3 * h + r) * M3_IMS;
-  // forward, class r: x'[i + 10 j] W^(r (i + 10 j)), radix 10 over j, then over i
-  float2 F[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int n = i + 10 * j;
-    const float2 x = col[(size_t)n * CB];
-    F[j] = r ? cmul(x, tw[r * n]) : x;
-  }
-  dft10<false>(F);
-  if (act) {
-#pragma unroll
-    for (int q = 0; q < 10; ++q) img[10 * i + q] = F[q];
-  }
-  wf::wave_sync();
-#pragma unroll
-  for (int j = 0; j < 10; ++j) F[j] = img[i + 10 * j];
-#pragma unroll
-  for (int j = 1; j < 10; ++j) F[j] = cmul(F[j], tw[3 * i * j]);
-  dft10<false>(F);  // F[q] = X_r[i + 10 q] (w3^r dropped, see above)
-  // spectrum element q is k = 3 (i + 10 q) + r
-  const size_t tc = (size_t)(bc % a.C) * a.ncols + c;
-  const int* mzc = a.mzt + tc * a.nz;
-  const float* sqc = a.sqt + tc * PN;
-  for (int zz = z_lo; zz < z_hi; ++zz) {
-    const float z = a.zv[a.zoff + zz];
-    const int M = mzc[zz];
-    int ii = i;
-    asm volatile("" : "+v"(ii));
-    float2 gz[10];
-    float2 (&g)[10] = ONEZ ? F : gz;
-#pragma unroll
-    for (int q = 0; q < 10; ++q) {
-      const int k = 3 * (ii + 10 * q) + r;
-      const int mx = freq_index(k, PN);
-      if (mx > M || -mx > M) {
-        g[q] = make_float2(0.f, 0.f);
-        continue;
-      }
-      // sqrt(k^2 - K^2) read per z from the column table (L2-resident; the layers run one z, and ten
-      // registers held across the loop push the kernel below 8 waves / SIMD)
-      float sn, cs;
-      sincos_hw(tf_mul(z, sqc[k]), &sn, &cs);
-      g[q] = cmul(F[q], make_float2(cs, a.adjoint ? -sn : sn));
-    }
-    // inverse, class r: radix 10 over q (inputs k' = i + 10 q), then over i
-    dft10<true>(g);
-    wf::wave_sync();  // the previous z's class-sum reads of the images are done
-    if (act) {
-#pragma unroll
-      for (int q = 0; q < 10; ++q) img[10 * ii + q] = g[q];
-    }
-    wf::wave_sync();
-#pragma unroll
-    for (int j = 0; j < 10; ++j) g[j] = img[ii + 10 * j];
-    {
-      // w100^(i j) by products of w100^i (one table load; the 19 loads of direct lookups would be
-      // issued together and held in registers)
-      const float2 w1 = tw[3 * ii];
-      float2 wj = w1;
-#pragma unroll
-      for (int j = 1; j < 10; ++j) {
-        g[j] = cmulc(g[j], wj);
-        if (j < 9) wj = cmul(wj, w1);
-      }
-    }
-    dft10<true>(g);  // g[q] = IDFT_100(Y_r)[m'], m' = i + 10 q
-    wf::wave_sync();
-    if (act) {
-      // W^(r m') = W^(r i) (W^(10 r))^q
-      const float2 st = tw[10 * r];
-      float2 wq = tw[r * ii];
-#pragma unroll
-      for (int q = 0; q < 10; ++q) {
-        img[ii + 10 * q] = cmulc(g[q], wq);
-        if (q < 9) wq = cmul(wq, st);
-      }
-    }
-    wf::wave_sync();
-    // the class sum of the 2 x 100 kept rows: output o = lane + 64 t
-    float2* dst = U + ((size_t)zz * a.BC + bc) * a.ncbu * CBU * a.Hout;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int o = lane + 64 * t;
-      if (o >= 2 * M3_L) continue;
-      const int hh = o >= M3_L, m = o - M3_L * hh;
-      const int cc = 2 * pr + hh;
-      const float2* s0 = lds + 3 * hh * M3_IMS + m;
-      const float2 v = cadd(cadd(s0[0], s0[M3_IMS]), s0[2 * M3_IMS]);
-      if (cc < a.ncols) dst[blk_u(cc, m, a.Hout)] = cscale(v, a.scale);
-    }
-  }
-}
-
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8)))
-asm_cols_m3(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
-  asm_cols_m3_body<true>(T, U, ph, a);
-}
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5)))
-asm_cols_m3_z(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
-  asm_cols_m3_body<false>(T, U, ph, a);
-}
-
-// The row passes of the same geometry (Pw = 300, input columns [100, 200) for K1, output columns
-// [100, 200) for K3) on the same 3 x 100 split, two rows per wave (lane = 32 half + 10 r + i).
-// K1: the 100 inputs of a row are formed once (lane e of the half takes elements e + 30 t: the fused
-// DOE modulation / loss-gradient loaders run once per element) and staged in LDS, then each class
-// r runs its pre-twiddle and 100-point forward, storing the band columns of k = 3 k' + r.
-// K3: each class gathers its band columns k = 3 k' + r, runs the 100-point inverse and its
-// post-twiddle; the class sum gives the 100 kept outputs of the row.
-constexpr size_t m3_rows_fwd_lds_bytes() { return (size_t)(2 * M3_L + 6 * M3_IMS) * sizeof(float2); }
-
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8)))
-asm_rows_fwd_m3(const float2* __restrict__ in, float2* __restrict__ T, FftPlan pw, AsmArgs a) {
-  constexpr int PN = 3 * M3_L;
-  extern __shared__ float2 lds[];
-  const int nblk = gridDim.x - a.tab_blocks;
-  if ((int)blockIdx.x >= nblk) {  // the column pass's tables of the first z-chunk, as asm_rows_fwd
-    tf_tables_body<PN>(a, blockIdx.x - nblk, 1);
-    return;
-  }
-  const int rows = (a.zsum ? a.nz : 1) * a.BC * a.Hin;
-  const int lane = threadIdx.x, h = lane >> 5, rem = lane & 31;
-  const bool act = rem < 30;
-  const int r = act ? rem / 10 : 0, i = act ? rem - 10 * r : 0;
-  const int row = 2 * (int)blockIdx.x + h;
-  const bool live = row < rows;
-  const int rw = live ? row : rows - 1;
-  const int plane = rw / a.Hin, hr = rw - plane * a.Hin;
-  const RowSrc<true> fetch(a, in, plane, hr);
-  float2* rowbuf = lds + h * M3_L;
-  if (live && act) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int e = rem + 30 * t;
-      if (e < M3_L) rowbuf[e] = fetch(e);
-    }
-  }
-  wf::wave_sync();
-  const float2* __restrict__ tw = pw.tw;
-  float2 F[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int n = i + 10 * j;
-    const float2 x = rowbuf[n];
-    F[j] = r ? cmul(x, tw[r * n]) : x;
-  }
-  dft10<false>(F);
-  float2* img = lds + 2 * M3_L + (3 * h + r) * M3_IMS;
-  if (act) {
-#pragma unroll
-    for (int q = 0; q < 10; ++q) img[10 * i + q] = F[q];
-  }
-  wf::wave_sync();
-#pragma unroll
-  for (int j = 0; j < 10; ++j) F[j] = img[i + 10 * j];
-#pragma unroll
-  for (int j = 1; j < 10; ++j) F[j] = cmul(F[j], tw[3 * i * j]);
-  dft10<false>(F);  // X[3 (i + 10 q) + r] = w3^r F[q]
-  if (!(live && act)) return;
-  const float2 w3r = r ? tw[M3_L * r] : make_float2(1.f, 0.f);  // w3^r = W^(100 r)
-  float2* dst = T + (size_t)plane * a.ncb * CB * a.Hin;
-#pragma unroll
-  for (int q = 0; q < 10; ++q) {
-    const int c = band_col(3 * (i + 10 * q) + r, PN, a.J, a.ncols);
-    if (c >= 0) dst[blk(c, hr, a.Hin)] = r ? cmul(F[q], w3r) : F[q];
-  }
-}
-
-template <bool LOSS>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(8)))
-asm_rows_inv_m3(const float2* __restrict__ U, float2* __restrict__ out, FftPlan pw, AsmArgs a) {
-  constexpr int PN = 3 * M3_L;
-  extern __shared__ float2 lds[];
-  const int rows = a.nz * a.BC * a.Hout;
-  const int lane = threadIdx.x, h = lane >> 5, rem = lane & 31;
-  const bool act = rem < 30;
-  const int r = act ? rem / 10 : 0, i = act ? rem - 10 * r : 0;
-  const int row = 2 * (int)blockIdx.x + h;
-  const int rw = row < rows ? row : rows - 1;
-  const int plane = rw / a.Hout, ro = rw - plane * a.Hout;
-  const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
-  const float2* __restrict__ tw = pw.tw;
-  // class r: Y[3 (i + 10 j) + r] (zero outside the band), the w3^-r of the class folded in
-  float2 g[10];
-#pragma unroll
-  for (int j = 0; j < 10; ++j) {
-    const int c = band_col(3 * (i + 10 * j) + r, PN, a.J, a.ncols);
-    g[j] = c >= 0 ? src[blk_u(c, ro, a.Hout)] : make_float2(0.f, 0.f);
-  }
-  dft10<true>(g);
-  float2* img = lds + (3 * h + r) * M3_IMS;
-  if (act) {
-#pragma unroll
-    for (int q = 0; q < 10; ++q) img[10 * i + q] = g[q];
-  }
-  wf::wave_sync();
-#pragma unroll
-  for (int j = 0; j < 10; ++j) g[j] = img[i + 10 * j];
-  {
-    const float2 w1 = tw[3 * i];
-    float2 wj = w1;
-#pragma unroll
-    for (int j = 1; j < 10; ++j) {
-      g[j] = cmulc(g[j], wj);
-      if (j < 9) wj = cmul(wj, w1);
-    }
-  }
-  dft10<true>(g);  // IDFT_100 of the class, m' = i + 10 q
-  wf::wave_sync();
-  if (act) {
-    // w3^-r W^(-r m') = W^(-r (100 + m')): one table entry and its steps W^(-10 r)
-    const float2 st = tw[10 * r];
-    float2 wq = tw[r * (M3_L + i)];
-#pragma unroll
-    for (int q = 0; q < 10; ++q) {
-      img[i + 10 * q] = cmulc(g[q], wq);
-      if (q < 9) wq = cmul(wq, st);
-    }
-  }
-  wf::wave_sync();
-  // the class sum of the 2 x 100 outputs: output o = lane + 64 t (row o / 100)
-  LossAcc acc[2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int o = lane + 64 * t;
-    if (o >= 2 * M3_L) continue;
-    const int hh = o >= M3_L, w = o - M3_L * hh;
-    const int rr = 2 * (int)blockIdx.x + hh;
-    if (rr >= rows) continue;
-    const int pl = rr / a.Hout, rout = rr - pl * a.Hout;
-    const float2* s0 = lds + 3 * hh * M3_IMS + w;
-    float2 v = cadd(cadd(s0[0], s0[M3_IMS]), s0[2 * M3_IMS]);  // (1 / (Ph Pw) applied by K2)
-    if (a.ap_side == 1 && !aperture_open(a.apm, rout, w)) v = cscale(v, 0.f);  // window mask (forward)
-    out[((size_t)(a.zoff * a.BC + pl) * a.Hout + rout) * a.Wout + w] = v;
-    if constexpr (LOSS) {
-      const int lb = pl / a.C, lc = pl - lb * a.C;
-      const int tb = a.ls.tB == 1 ? 0 : lb, tc = a.ls.tC == 1 ? 0 : lc;
-      const float tv = a.ls.target[(((size_t)tb * a.ls.tC + tc) * a.Hout + rout) * a.Wout + w];
-      acc[hh].add(v, tv, (unsigned)((lc * a.Hout + rout) * a.Wout + w));
-    }
-  }
-  if constexpr (LOSS) {
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int rr = 2 * (int)blockIdx.x + hh;
-      if (rr >= rows) continue;  // uniform over the workgroup
-      const int pl = rr / a.Hout, rout = rr - pl * a.Hout;
-      const int lb = pl / a.C, lc = pl - lb * a.C;
-      loss_store_part(acc[hh], a.ls, lb, lc * a.Hout + rout);  // the slot of asm_rows_inv_loss
-    }
-  }
 }
 
 template <class MP>
@@ -1590,7 +815,7 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
   const int row = xcd_rows(blockIdx.x, gridDim.x);  // row in [0, nz*BC*Hout)
   const int plane = row / a.Hout, r = row - plane * a.Hout;  // plane = zz*BC + bc
   const int tid = threadIdx.x, nt = blockDim.x;
-  const float2* src = U + (size_t)plane * a.ncbu * CBU * a.Hout;
+  const float2* src = U + (size_t)plane * a.ncbu * CBU * u_rows(a.Hout);
   float2* dst = out + ((size_t)(a.zoff * a.BC + plane) * a.Hout + r) * a.Wout;
   LossAcc acc;
   const float* trow = nullptr;
@@ -1646,7 +871,8 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     static_assert(NB0 % CBU == 0, "band offsets must be whole U blocks");
     static_assert(Geo<PN>::T == NB0, "one first-stage butterfly per thread: i = tid");
     const int c0 = tid + a.J;
-    const float2* base = src + ((long)(c0 / CBU) * a.Hout + r) * CBU + (c0 % CBU);
+    const float2* base = src + blk_u(c0, r, a.Hout);
+    const long cstride = u_rows(a.Hout);  // blk_u(c + delta) - blk_u(c) = delta * cstride for CBU | delta
     // operands q in [4, 12) are the columns PN/4 <= |m_y| < 3 PN/4: outside the band for every
     // lane of most waves (all but the first and last at cfg2), which then skip their address math
     // and masked loads on one scalar branch
@@ -1656,7 +882,7 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
       if (q >= 4 && q < 12 && mid0) return make_float2(0.f, 0.f);
       const int delta = q * NB0 >= PN / 2 ? q * NB0 - PN : q * NB0;
       if ((unsigned)(c0 + delta) >= (unsigned)a.ncols) return make_float2(0.f, 0.f);
-      return base[(long)delta * a.Hout];
+      return base[(long)delta * cstride];
     };
     auto sv = [&](int, int, int j, float2 v) {
       const int w = j - (MID ? PN / 4 : a.out_c0);
@@ -1801,7 +1027,7 @@ static int validate(const thz_asm_desc* d) {
   if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d wavelengths", d->C, THZ_MAX_WAVELENGTHS);
   if (d->Z < 1 || d->Z > THZ_MAX_Z) return fail(THZ_E_UNSUPPORTED, "Z=%d outside [1, %d]", d->Z, THZ_MAX_Z);
   if (d->bandlimit < 0 || d->bandlimit > 2) return fail(THZ_E_ARG, "bad bandlimit %d", d->bandlimit);
-  if (!d->wavelengths || !d->z) return fail(THZ_E_ARG, "null wavelengths / z");
+  if (!d->wavelengths || (!d->z && !d->z_dev)) return fail(THZ_E_ARG, "null wavelengths / z");
   if (!(d->dx > 0.f) || !(d->dy > 0.f)) return fail(THZ_E_ARG, "spacing must be > 0");
   const int Ph = d->H + 2 * d->pad_h, Pw = d->W + 2 * d->pad_w;
   if (Ph > FFT_MAX_N || Pw > FFT_MAX_N)
@@ -1821,8 +1047,12 @@ static int band_half_width(const thz_asm_desc* d, int Ph, int Pw) {
     const double lam = d->wavelengths[c];
     const double kl = 2.0 * M_PI / lam;
     for (int zi = 0; zi < d->Z; ++zi) {
-      const double z = d->z[zi];
       double lim = kl;
+      if (d->z_dev) {  // the planes are read on the device: size the band for any z (evanescent bound)
+        kymax = std::max(kymax, lim);
+        continue;
+      }
+      const double z = d->z[zi];
       if (d->bandlimit == THZ_BANDLIMIT_EXACT) {
         const double dv = 1.0 / (2.0 * Ph * dy);
         const double vl = 1.0 / std::sqrt(std::pow(2.0 * dv * z, 2) + 1.0) / lam;
@@ -1900,12 +1130,7 @@ template <int PN>
 static void add_kernels(std::vector<const void*>& ks) {
   ks.push_back((const void*)asm_rows_fwd<PN>);
   ks.push_back((const void*)asm_cols<PN>);
-  if constexpr (PN == 8192) {
-    ks.push_back((const void*)asm_cols_mid<PN>);
-    ks.push_back((const void*)asm_cols_range<PN>);
-    ks.push_back((const void*)asm_cols_ord<PN>);
-    ks.push_back((const void*)asm_rows_inv_mid<PN>);
-  }
+  if constexpr (PN == 8192) ks.push_back((const void*)asm_rows_inv_mid<PN>);
   ks.push_back((const void*)asm_cols_zsum<PN>);
   ks.push_back((const void*)asm_rows_inv<PN>);
   ks.push_back((const void*)asm_rows_inv_loss<PN>);
@@ -1931,31 +1156,6 @@ static int ensure_lds_attr() {
       hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx);
       if (e != hipSuccess) err = e;
     }
-    const int mxp = (int)(2 * lds_floats2(8192) + tw_lds_count(8192)) * (int)sizeof(float2) + 2 * 4 * THZ_MAX_Z;
-    const hipError_t e = hipFuncSetAttribute((const void*)asm_cols_pair<8192>,
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, mxp);
-    if (e != hipSuccess) err = e;
-    const hipError_t eh = hipFuncSetAttribute((const void*)asm_cols_pair_hb<8192>,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, mxp + 8);
-    if (eh != hipSuccess) err = eh;
-    const hipError_t e4 = hipFuncSetAttribute((const void*)asm_cols_4s, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)fs::lds_bytes(THZ_MAX_Z));
-    if (e4 != hipSuccess) err = e4;
-    const hipError_t e6 = hipFuncSetAttribute((const void*)asm_cols_4s_pair,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)fs::lds_bytes(THZ_MAX_Z, 2));
-    if (e6 != hipSuccess) err = e6;
-    const hipError_t e7 = hipFuncSetAttribute((const void*)asm_cols_4s_pair_hb,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)fs::lds_bytes(THZ_MAX_Z, 2) + 8);
-    if (e7 != hipSuccess) err = e7;
-    const hipError_t e8 = hipFuncSetAttribute((const void*)asm_cols_4s_pair_hb2,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize,
-                                              (int)fs::lds_bytes(THZ_MAX_Z, 2) + 8);
-    if (e8 != hipSuccess) err = e8;
-    const hipError_t e5 = hipFuncSetAttribute((const void*)asm_rows_inv_4s,
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)k3_4s_lds_bytes());
-    if (e5 != hipSuccess) err = e5;
   });
   if (err != hipSuccess) return fail(THZ_E_HIP, "hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s",
                                      hipGetErrorString(err));
@@ -1972,123 +1172,29 @@ static int mx_kind(int n) { return is_mx(n) ? n : 0; }
   if (mx_kind(n) == Mx300::N) hipLaunchKernelGGL(KER<Mx300::N>, G, dim3(MX_T), LDSB, __VA_ARGS__); \
   else THZ_POW2_SWITCH(n, KER, G, dim3(threads_for(n)), LDSB, __VA_ARGS__)
 
-// Paired-column K2 (asm_cols_pair) at Ph = 8192, opt-in with THZ_K2_PAIR=1: 2 x 512 threads, two
-// 70 KB LDS images, 127 VGPRs without spills (the 2048 / 4096 pairs spill a few).  Measured on
-// cfg2 (profiles/r03_k2_pair_experiment.txt): its U writes are exactly U (WRITE_SIZE 8.62 GB per
-// launch against 14.47 GB for the one-column kernel), but one 16-wave workgroup per CU stalls at
-// every barrier where two 8-wave workgroups overlap theirs: 4.39 ms against 4.16 ms.  The pass is
-// issue-bound, not write-bound, so the one-column kernel stays the default.
-// THZ_K2_PAIR=2: asm_cols_pair_hb, the same kernel with per-half LDS-counter barriers in the
-// per-plane inverse and one workgroup barrier per plane.  Returns 0, 1 or 2.
-static int k2_pair(int Ph) {
-  static const int mode = [] {
-    const char* e = getenv("THZ_K2_PAIR");
-    return e && e[0] == '1' ? 1 : e && e[0] == '2' ? 2 : 0;
-  }();
-  return Ph == 8192 ? mode : 0;
-}
-// Four-step K2 (asm_cols_4s) at Ph = 8192 for the analytic transfer function (ASM forward and
-// adjoint of one z-chunk); THZ_K2_4S=0 selects the three-stage asm_cols, THZ_K2_4S=2 the paired
-// asm_cols_4s_pair (A/B switches).  Returns 0 (off), 1 or 2 (columns per workgroup).
-static int k2_4s(int Ph, const AsmArgs& a) {
-  static const int mode = [] {
-    const char* e = getenv("THZ_K2_4S");
-    return e && e[0] >= '1' && e[0] <= '4' ? e[0] - '0' : 0;
-  }();
-  return Ph == fs::N && !a.tft && !a.zsum ? mode : 0;
-}
-// K2 at Ph = 8192 with the middle-half crop of padding scale 1 (cfg2): asm_cols_mid, the crop a
-// compile-time window: opt-in THZ_K2_MID=1 (measured 4.34-4.39 vs 4.19-4.22 ms on cfg2 with 10 % fewer
-// VALU instructions per plane: not the default)
-static bool k2_mid(int Ph, const AsmArgs& a) {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K2_MID");
-    return e && e[0] == '1';
-  }();
-  return on && Ph == 8192 && !a.tft && !a.zsum && a.out_r0 == Ph / 4 && a.Hout == Ph / 2;
-}
-static bool k2_ord(int Ph, const AsmArgs& a) {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K2_ORD");
-    return e && e[0] == '1';
-  }();
-  return on && Ph == 8192 && !a.tft && !a.zsum;
-}
-static bool k2_range(int Ph, const AsmArgs& a) {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K2_RANGE");
-    return e && e[0] == '1';
-  }();
-  return on && Ph == 8192 && !a.tft && !a.zsum;
-}
-// the 300-point passes with the layers' windows as constants: THZ_MX_MID=0 selects the generic
-// kernels (A/B); 2 keeps the constants in the column pass only
-static int mx_mid_mode() {
-  static const int mode = [] {
-    const char* e = getenv("THZ_MX_MID");
-    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
-  }();
-  return mode;
-}
-static bool mx_mid_on() { return mx_mid_mode() == 1; }
-// the column pass (asm_cols_mx_mid, the default: 80.8 vs 83.3 us per launch, cfg5 chained 1.097
-// vs 1.133 ms)
+// The 300-point passes with the layers' windows ([N/3, 2N/3) in and out: padding 2 with unpad,
+// cfg4 / cfg5) as compile-time constants: the column pass (asm_cols_mx_mid: 80.8 vs 83.3 us per
+// launch, cfg5 chained 1.097 vs 1.133 ms), K1 (asm_rows_fwd<300, true>) and K3
+// (asm_rows_inv_mid<300>, asm_rows_inv_loss_mid<300>).  The A/B records: profiles/r04_experiments.txt.
 static bool mx_mid(const AsmArgs& a) {
-  const bool on = mx_mid_mode() != 0;
-  return on && !a.tft && a.in_r0 == Mx300::N / 3 && a.Hin == Mx300::N / 3 && a.out_r0 == Mx300::N / 3 &&
+  return !a.tft && a.in_r0 == Mx300::N / 3 && a.Hin == Mx300::N / 3 && a.out_r0 == Mx300::N / 3 &&
          a.Hout == Mx300::N / 3;
 }
-// K3 at Pw = 8192 with the middle-half crop (asm_rows_inv_mid, the default: 4.00 vs 4.13 ms on cfg2;
-// THZ_K3_MID=0 selects asm_rows_inv<8192>)
+// K3 with its crop as a compile-time window: the middle half of P = 8192 (asm_rows_inv_mid<8192>,
+// padding scale 1 with unpad, cfg2: 4.00 vs 4.13 ms) or the middle third of P = 300
 static bool k3_mid(int Pw, const AsmArgs& a) {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K3_MID");
-    return !(e && e[0] == '0');
-  }();
-  return (on && Pw == 8192 && a.out_c0 == Pw / 4 && a.Wout == Pw / 2) ||
-         (mx_mid_on() && Pw == Mx300::N && a.out_c0 == Pw / 3 && a.Wout == Pw / 3);
+  return (Pw == 8192 && a.out_c0 == Pw / 4 && a.Wout == Pw / 2) ||
+         (Pw == Mx300::N && a.out_c0 == Pw / 3 && a.Wout == Pw / 3);
 }
 // K1 of the 300-point layers with the input window as constants (asm_rows_fwd<300, true>)
-static bool k1_mid(int Pw, const AsmArgs& a) {
-  return mx_mid_on() && Pw == Mx300::N && a.in_c0 == Pw / 3 && a.Win == Pw / 3;
-}
-// Four-step K3 (asm_rows_inv_4s) at Pw = 8192, opt-in THZ_K3_4S=1 (A/B against asm_rows_inv<8192>).
-static bool k3_4s(int Pw) {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K3_4S");
-    return e && e[0] == '1';
-  }();
-  return on && Pw == fs::N;
-}
-
-// The 3 x 100 row passes (asm_rows_fwd_m3 / asm_rows_inv_m3) at Pw = 300 with the input (K1) or
-// output (K3) columns [100, 200); THZ_K2_M3=0 selects the 5 3 4 5 row kernels too.
-static bool m3_on() {
-  static const bool on = [] {
-    const char* e = getenv("THZ_K2_M3");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-static bool k1_m3(int Pw, const AsmArgs& a) { return m3_on() && Pw == 3 * M3_L && a.in_c0 == M3_L && a.Win == M3_L; }
-static bool k3_m3(int Pw, const AsmArgs& a) { return m3_on() && Pw == 3 * M3_L && a.out_c0 == M3_L && a.Wout == M3_L; }
-
-// The 3 x 100 column pass (asm_cols_m3) at Ph = 300 with both windows [100, 200) (cfg4 / cfg5
-// layers), analytic transfer function; THZ_K2_M3=0 selects the 5 3 4 5 asm_cols_mx (A/B switch).
-static bool k2_m3(int Ph, const AsmArgs& a) {
-  return m3_on() && Ph == 3 * M3_L && !a.tft && !a.zsum && a.in_r0 == M3_L && a.Hin == M3_L && a.out_r0 == M3_L &&
-         a.Hout == M3_L;
-}
-static size_t k2_pair_lds(int Ph) {
-  return (size_t)(2 * lds_floats2(Ph) + tw_lds_count(Ph)) * sizeof(float2) + 2 * 4 * THZ_MAX_Z;
-}
-static int k2_resident(int Ph, bool pair, int threads, size_t lds, const void* kern = nullptr) {
+static bool k1_mid(int Pw, const AsmArgs& a) { return Pw == Mx300::N && a.in_c0 == Pw / 3 && a.Win == Pw / 3; }
+static int k2_resident(int Ph, int threads, size_t lds) {
   static std::mutex mu;
-  static std::map<std::tuple<int, int, bool, const void*, int, size_t>, int> cache;
+  static std::map<std::tuple<int, int, int, size_t>, int> cache;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
   std::lock_guard<std::mutex> lk(mu);
-  auto key = std::make_tuple(dev, Ph, pair, kern, threads, lds);
+  auto key = std::make_tuple(dev, Ph, threads, lds);
   auto it = cache.find(key);
   if (it != cache.end()) return it->second;
   const void* k = nullptr;
@@ -2096,12 +1202,11 @@ static int k2_resident(int Ph, bool pair, int threads, size_t lds, const void* k
     case 1024: k = (const void*)asm_cols<1024>; break;
     case 2048: k = (const void*)asm_cols<2048>; break;
     case 4096: k = (const void*)asm_cols<4096>; break;
-    case 8192: k = pair ? (const void*)asm_cols_pair<8192> : (const void*)asm_cols<8192>; break;
+    case 8192: k = (const void*)asm_cols<8192>; break;
     case 16384: k = (const void*)asm_cols<16384>; break;
     default: k = (const void*)asm_cols<0>; break;
   }
   if (mx_kind(Ph) == Mx300::N) k = (const void*)asm_cols_mx<Mx300>;
-  if (kern) k = kern;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -2112,12 +1217,9 @@ static int k2_resident(int Ph, bool pair, int threads, size_t lds, const void* k
 }
 
 // K2 task split: whole columns for the full dispatch rounds, the remainder split by z-range.
-// pair: two columns per task (asm_cols_pair, asm_cols_m3); kern: the kernel, when not the default
-// of its size
-static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds, bool pair = false,
-                    const void* kern = nullptr) {
-  const int nc = (pair ? (g.ncols + 1) / 2 : g.ncols) * g.BC;
-  const int G = k2_resident(g.Ph, pair, threads, lds, kern);
+static int k2_tasks(const AsmGeom& g, AsmArgs* a, int threads, size_t lds) {
+  const int nc = g.ncols * g.BC;
+  const int G = k2_resident(g.Ph, threads, lds);
   if (G <= 0 || a->nz <= 1) {
     a->kfull = nc;
     a->kparts = 1;
@@ -2138,7 +1240,7 @@ static size_t t_bytes(const AsmGeom& g) {
   return align256((size_t)(g.adj ? g.zc : 1) * g.BC * g.ncb * CB * g.Hin * sizeof(float2));
 }
 static size_t ws_bytes(const AsmGeom& g) {
-  return t_bytes(g) + align256((size_t)(g.adj ? 1 : g.zc) * g.BC * g.ncbu * CBU * g.Hout * sizeof(float2)) +
+  return t_bytes(g) + align256((size_t)(g.adj ? 1 : g.zc) * g.BC * g.ncbu * CBU * u_rows(g.Hout) * sizeof(float2)) +
          tab_bytes(g);
 }
 
@@ -2157,10 +1259,7 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
     a.zacc = z0 > 0;
     {
       KernelTimer kt("asm_rows_fwd", s);
-      if (k1_m3(g.Pw, a)) {
-        hipLaunchKernelGGL(asm_rows_fwd_m3, dim3((a.nz * g.BC * g.Hin + 1) / 2), dim3(64), m3_rows_fwd_lds_bytes(), s,
-                           (const float2*)in, T, pw, a);
-      } else if (k1_mid(g.Pw, a)) {
+      if (k1_mid(g.Pw, a)) {
         hipLaunchKernelGGL((asm_rows_fwd<Mx300::N, true>), dim3(a.nz * g.BC * g.Hin), dim3(MX_T), fft_lds_bytes_io(g.Pw),
                            s, (const float2*)in, T, pw, a);
       } else {
@@ -2191,13 +1290,8 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
   a.nz = 1;
   {
     KernelTimer kt("asm_rows_inv", s);
-    if (k3_m3(g.Pw, a)) {
-      hipLaunchKernelGGL(asm_rows_inv_m3<false>, dim3((g.BC * g.Hout + 1) / 2), dim3(64), m3_lds_bytes(), s,
-                         (const float2*)U, (float2*)out, pw, a);
-    } else {
-      THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
-                      (float2*)out, pw, a);
-    }
+    THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
+                    (float2*)out, pw, a);
     THZ_LAUNCH_CHECK();
     kt.stop();
   }
@@ -2223,10 +1317,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     KernelTimer kt("asm_rows_fwd", s);
     a.zoff = 0;
     a.nz = std::min(g.zc, Z);
-    if (k1_m3(g.Pw, a)) {
-      hipLaunchKernelGGL(asm_rows_fwd_m3, dim3((g.BC * g.Hin + 1) / 2 + a.tab_blocks), dim3(64),
-                         m3_rows_fwd_lds_bytes(), s, (const float2*)in, T, pw, a);
-    } else if (k1_mid(g.Pw, a)) {
+    if (k1_mid(g.Pw, a)) {
       hipLaunchKernelGGL((asm_rows_fwd<Mx300::N, true>), dim3(g.BC * g.Hin + a.tab_blocks), dim3(MX_T),
                          fft_lds_bytes_io(g.Pw), s, (const float2*)in, T, pw, a);
     } else {
@@ -2247,57 +1338,13 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
           THZ_LAUNCH_CHECK();
         }
       }
-      if (k2_m3(g.Ph, a)) {
-        const void* kern = a.nz == 1 ? (const void*)asm_cols_m3 : (const void*)asm_cols_m3_z;
-        const int ntask = k2_tasks(g, &a, 64, m3_lds_bytes(), true, kern);
-        if (a.nz == 1)
-          hipLaunchKernelGGL(asm_cols_m3, dim3(ntask), dim3(64), m3_lds_bytes(), s, (const float2*)T, U, ph, a);
-        else
-          hipLaunchKernelGGL(asm_cols_m3_z, dim3(ntask), dim3(64), m3_lds_bytes(), s, (const float2*)T, U, ph, a);
-      } else if (mx_kind(g.Ph) == Mx300::N) {
+      if (mx_kind(g.Ph) == Mx300::N) {
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, MX_T, lds2);
         if (mx_mid(a))
           hipLaunchKernelGGL(asm_cols_mx_mid<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
         else
           hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
-      } else if (const int m4 = k2_4s(g.Ph, a)) {
-        // LDS for the largest chunk of this call (the resident count must not depend on the chunk)
-        const int nc4 = m4 >= 2 ? 2 : 1;
-        const size_t lds2 = fs::lds_bytes(std::min(g.zc, Z), nc4) + (m4 >= 3 ? 8 : 0);
-        const void* kern = m4 == 4   ? (const void*)asm_cols_4s_pair_hb2
-                           : m4 == 3 ? (const void*)asm_cols_4s_pair_hb
-                           : m4 == 2 ? (const void*)asm_cols_4s_pair
-                                     : (const void*)asm_cols_4s;
-        const int ntask = k2_tasks(g, &a, nc4 * fs::T, lds2, nc4 == 2, kern);
-        if (m4 == 4)
-          hipLaunchKernelGGL(asm_cols_4s_pair_hb2, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
-        else if (m4 == 3)
-          hipLaunchKernelGGL(asm_cols_4s_pair_hb, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
-        else if (m4 == 2)
-          hipLaunchKernelGGL(asm_cols_4s_pair, dim3(ntask), dim3(2 * fs::T), lds2, s, (const float2*)T, U, ph, a);
-        else
-          hipLaunchKernelGGL(asm_cols_4s, dim3(ntask), dim3(fs::T), lds2, s, (const float2*)T, U, ph, a);
-      } else if (const int pm = k2_pair(g.Ph)) {
-        const size_t lds2 = k2_pair_lds(g.Ph) + (pm == 2 ? 8 : 0);
-        const int ntask = k2_tasks(g, &a, 2 * th, lds2, true,
-                                   pm == 2 ? (const void*)asm_cols_pair_hb<8192> : (const void*)asm_cols_pair<8192>);
-        if (pm == 2)
-          hipLaunchKernelGGL(asm_cols_pair_hb<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
-        else
-          hipLaunchKernelGGL(asm_cols_pair<8192>, dim3(ntask), dim3(2 * th), lds2, s, (const float2*)T, U, ph, a);
-      } else if (k2_ord(g.Ph, a)) {
-        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_ord<8192>);
-        hipLaunchKernelGGL(asm_cols_ord<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
-      } else if (k2_range(g.Ph, a)) {
-        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_range<8192>);
-        hipLaunchKernelGGL(asm_cols_range<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
-      } else if (k2_mid(g.Ph, a)) {
-        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-        const int ntask = k2_tasks(g, &a, th, lds2, false, (const void*)asm_cols_mid<8192>);
-        hipLaunchKernelGGL(asm_cols_mid<8192>, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         const int ntask = k2_tasks(g, &a, th, lds2);
@@ -2308,13 +1355,8 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     }
     {
       KernelTimer kt("asm_rows_inv", s);
-      const bool m3 = k3_m3(g.Pw, a);
-      const dim3 g3((a.nz * g.BC * g.Hout + 1) / 2);
       if (a.ls.stats) {
-        if (m3) {
-          hipLaunchKernelGGL(asm_rows_inv_m3<true>, g3, dim3(64), m3_lds_bytes(), s, (const float2*)U, (float2*)out,
-                             pw, a);
-        } else if (g.Pw == Mx300::N && k3_mid(g.Pw, a)) {
+        if (g.Pw == Mx300::N && k3_mid(g.Pw, a)) {
           hipLaunchKernelGGL(asm_rows_inv_loss_mid<Mx300::N>, dim3(a.nz * g.BC * g.Hout), dim3(MX_T),
                              fft_lds_bytes_io(g.Pw), s, (const float2*)U, (float2*)out, pw, a);
         } else {
@@ -2323,12 +1365,6 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         }
         THZ_LAUNCH_CHECK();
         if ((e = launch_loss_finish(a.ls, s))) return e;
-      } else if (m3) {
-        hipLaunchKernelGGL(asm_rows_inv_m3<false>, g3, dim3(64), m3_lds_bytes(), s, (const float2*)U, (float2*)out, pw,
-                           a);
-      } else if (k3_4s(g.Pw)) {
-        hipLaunchKernelGGL(asm_rows_inv_4s, dim3((a.nz * g.BC * g.Hout + K3_RPW - 1) / K3_RPW), dim3(fs::T),
-                           k3_4s_lds_bytes(), s, (const float2*)U, (float2*)out, pw, a);
       } else if (k3_mid(g.Pw, a)) {
         if (g.Pw == 8192)
           hipLaunchKernelGGL(asm_rows_inv_mid<8192>, dim3(a.nz * g.BC * g.Hout), dim3(threads_for(8192)),
@@ -2413,7 +1449,9 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
   a.dy = d->dy;
   a.scale = (float)(1.0 / ((double)g.Ph * (double)g.Pw));
   for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
-  for (int zi = 0; zi < d->Z; ++zi) a.zv[zi] = d->z[zi];
+  if (d->z)
+    for (int zi = 0; zi < d->Z; ++zi) a.zv[zi] = d->z[zi];
+  a.zdev = d->z_dev;
   if (m) {
     a.mod_h = mh;
     a.mod_u = mu;
@@ -2435,8 +1473,8 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
     a.apm = aperture_args(w, Ho, Wo);
     a.ap_side = d->adjoint ? 2 : 1;
     // carried by the 300-point row passes only (the K3 storer forward, the K1 loader adjoint:
-    // asm_rows_inv<300> / asm_rows_fwd<300>, or their 3 x 100 forms)
-    if (mx_kind(g.Pw) != Mx300::N && (d->adjoint ? !k1_m3(g.Pw, a) : !k3_m3(g.Pw, a)))
+    // asm_rows_inv<300> / asm_rows_fwd<300>)
+    if (mx_kind(g.Pw) != Mx300::N)
       return fail(THZ_E_UNSUPPORTED, "window mask: only the 300-point row passes fold the aperture; "
                                      "apply it separately");
     if (d->adjoint && d->Z > 1)
@@ -2484,6 +1522,7 @@ extern "C" int thz_asm_transfer_function(const thz_asm_desc* d, void* out, thz_s
   int e = validate(d);
   if (e) return e;
   if (!out) return fail(THZ_E_ARG, "null output pointer");
+  if (!d->z) return fail(THZ_E_ARG, "the transfer-function table takes a host z");
   AsmGeom g;
   geometry(d, &g);
   AsmArgs a{};
@@ -2624,7 +1663,7 @@ static int rsc_plan(const thz_rsc_desc* d, RscPlan* p) {
   p->tk = align256((size_t)d->C * k.ncbK * CB * g.Ph * sizeof(float2));
   p->kf = align256((size_t)d->C * g.Pw * g.Ph * sizeof(float2));
   p->t = align256((size_t)g.BC * g.ncb * CB * g.Hin * sizeof(float2));
-  p->u = align256((size_t)g.BC * g.ncbu * CBU * g.Hout * sizeof(float2));
+  p->u = align256((size_t)g.BC * g.ncbu * CBU * u_rows(g.Hout) * sizeof(float2));
   return THZ_OK;
 }
 

@@ -38,8 +38,22 @@ constexpr int CBU = 4;
 __device__ __forceinline__ size_t blk(int c, int row, int rows) {
   return ((size_t)(c / CB) * rows + row) * CB + (c % CB);
 }
+#ifndef THZ_UL
+#define THZ_UL 0
+#endif
+// THZ_UL = 1 (A/B build): U in 4 x 4 tiles of (column, row) whose 32-B sectors are 4 consecutive ROWS
+// of one column -- the 128-B line holds the same 16 elements as the blocked layout, transposed --
+// so the column pass writes whole sectors itself and the row pass reads 8 B of each of 4 sectors.
+// U's rows are padded to a multiple of 4 (u_rows).
+__host__ __device__ constexpr int u_rows(int rows) { return THZ_UL ? (rows + 3) & ~3 : rows; }
 __device__ __forceinline__ size_t blk_u(int c, int row, int rows) {
+  if constexpr (THZ_UL) return ((size_t)(c / CBU) * u_rows(rows) + (row & ~3)) * CBU + (c % CBU) * 4 + (row & 3);
   return ((size_t)(c / CBU) * rows + row) * CBU + (c % CBU);
+}
+// offset of row r from row 0 of the same column of U
+__device__ __forceinline__ size_t u_roff(int r) {
+  if constexpr (THZ_UL) return (size_t)(r & ~3) * CBU + (r & 3);
+  return (size_t)r * CBU;
 }
 
 
@@ -273,13 +287,14 @@ __device__ __forceinline__ unsigned long long rng_bits(const unsigned* rng, unsi
 __device__ __forceinline__ float rng_u01(const unsigned* rng, unsigned stream, unsigned idx) {
   return (float)(unsigned)(rng_bits(rng, stream, idx) >> 40) * (1.0f / 16777216.0f);
 }
-// Exp(1) = -log U with U in (0, 1] (Tensor.exponential_)
-// Exp(1) = -log(u), u = (b + 1) / 2^24 in (0, 1].  The top bin (u = 1, probability 2^-24) gives
-// E = 0 and a Gumbel draw -log(E) = +inf, which turns gumbel_softmax into NaN (a 6,000-iteration
-// v3 / naive-Gumbel run draws ~10^7-10^8 values): E is held at 2^-25, the middle of that bin's range.
+// Exp(1) = -log(u), u = (b + 1) / 2^24 in (0, 1] (Tensor.exponential_).  The top bin (u = 1,
+// probability 2^-24) would give E = 0 and a Gumbel draw -log(E) = +inf, which turns gumbel_softmax
+// into NaN (a 6,000-iteration v3 / naive-Gumbel run draws ~10^7-10^8 values).  torch's CUDA
+// transformation::exponential maps every u >= 1 - eps/2 to log = -eps/2, i.e. E = 2^-24 for fp32;
+// the same floor here (u = 1 - 2^-24 already gives -logf(u) = 2^-24).
 __device__ __forceinline__ float rng_exp1(const unsigned* rng, unsigned stream, unsigned idx) {
   const float e = -logf((float)((unsigned)(rng_bits(rng, stream, idx) >> 40) + 1u) * (1.0f / 16777216.0f));
-  return fmaxf(e, 2.98023224e-8f);
+  return fmaxf(e, 5.96046448e-8f);
 }
 
 // noisy height at a source pixel: h + (u - 0.5) * 2 * tol  (:85); u == nullptr: the device

@@ -49,11 +49,15 @@ __host__ __device__ constexpr int lds_floats2(int n) { return n + (n >> 4) + 1; 
 // SIMD for both halves, and its aligned register pairs push the column pass into spills).
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+// The fused multiply-adds are written out: with a * b + c * d left to contraction, which product the
+// compiler keeps rounded differs between instantiations of one transform (a window folded as a
+// compile-time constant changed 10 % of the cfg2 outputs by an ulp), so every kernel that runs the
+// same butterflies now rounds them the same way.
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+  return make_float2(__builtin_fmaf(a.x, b.x, -(a.y * b.y)), __builtin_fmaf(a.x, b.y, a.y * b.x));
 }
 __device__ __forceinline__ float2 cmulc(float2 a, float2 b) {
-  return make_float2(a.x * b.x + a.y * b.y, a.y * b.x - a.x * b.y);
+  return make_float2(__builtin_fmaf(a.x, b.x, a.y * b.y), __builtin_fmaf(a.y, b.x, -(a.x * b.y)));
 }
 __device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
 __device__ __forceinline__ float2 add_mfwd(float2 a, float2 d) { return make_float2(a.x + d.y, a.y - d.x); }
@@ -448,15 +452,9 @@ __device__ __forceinline__ int stage_order(int tid) {
     return tid;
 }
 
-// the workgroup barrier of the exchanges (a caller may pass a narrower one, e.g. over one half of
-// a paired-column workgroup whose halves own separate images)
-struct SyncAll {
-  __device__ void operator()() const { __syncthreads(); }
-};
-
 template <int R, bool INV, int N, int L, int T, bool IN_LDS, bool OUT_LDS, int LIN = 1, int LOUT = L, class Tw,
-          class Ld, class Sv, class Bar = SyncAll>
-__device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv, Bar bar = Bar{}) {
+          class Ld, class Sv>
+__device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
   constexpr int NB = N / R;
   constexpr int MB = NB / T;  // butterflies per thread (exact)
   static_assert(MB * T == NB, "pow2 plan must tile exactly");
@@ -492,7 +490,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
     dftR<R, INV>(v[m]);
   }
   if constexpr (OUT_LDS) {
-    bar();
+    __syncthreads();
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
       const int i = bo + m * T;
@@ -502,7 +500,7 @@ __device__ __forceinline__ void stage_x(float2* lds, const Tw& tw, int tid, Ld& 
 #pragma unroll
       for (int r = 0; r < R; ++r) dst[c64_lay<LOUT>(j0 + r * L) - c64_lay<LOUT>(j0)] = v[m][r];
     }
-    bar();
+    __syncthreads();
   } else {
 #pragma unroll
     for (int m = 0; m < MB; ++m) {
@@ -572,9 +570,7 @@ __device__ __forceinline__ void swap_halves(float& a, float& b) {
   b = __int_as_float(r[1]);
 }
 
-// ORD = 1: the p-loop starts at p = 4 (for a centred half crop the kept rows then go out in
-// ascending order; an A/B of the store order's effect on the L2's sector merging, asm_cols_ord)
-template <bool INV, int N, int ORD = 0, class Tw, class Sv>
+template <bool INV, int N, class Tw, class Sv>
 __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float2 (&x)[16], Sv& sv) {
   constexpr int L = N / 32;
   // exp(-2 pi i q / 32) = (C32C[q], -C32S[q]), q < 16
@@ -620,8 +616,7 @@ __device__ __forceinline__ void stage_r32_pair_last(const Tw& tw, int tid, float
   const float2 wi = twat(tw, i);
   const float2 f = e ? cmul(wi, make_float2(C32C[1], -C32S[1])) : wi;  // w^i w32^e
 #pragma unroll
-  for (int pp = 0; pp < 8; ++pp) {
-    const int p = ORD ? (pp + 4) & 7 : pp;
+  for (int p = 0; p < 8; ++p) {
     float2 a = x[2 * p], b = x[2 * p + 1];
     swap_halves(a.x, b.x);
     swap_halves(a.y, b.y);
@@ -691,9 +686,9 @@ struct NoIO {
 
 // Stages S .. NST-1 of a power-of-two transform.  Stage 0 reads through ld unless
 // FIRST_LDS; the final stage writes through sv unless LAST_LDS.
-template <bool INV, int N, int T, int MODE, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1, int ORD = 0,
-          class Tw, class Ld, class Sv, class Bar = SyncAll>
-__device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv, Bar bar = Bar{}) {
+template <bool INV, int N, int T, int MODE, bool FIRST_LDS, bool LAST_LDS, int S = 0, int L = 1, class Tw, class Ld,
+          class Sv>
+__device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, Ld& ld, Sv& sv) {
   using P = Pow2Sched<N>;
   constexpr int NS = P::nst(MODE);
   if constexpr (S < NS) {
@@ -712,10 +707,10 @@ __device__ __forceinline__ void fft_pow2_io(float2* lds, const Tw& tw, int tid, 
       float2 x[16];
 #pragma unroll
       for (int s = 0; s < 16; ++s) x[s] = src[c64_lay<LIN>(2 * s * LP) - c64_lay<LIN>(0)];
-      stage_r32_pair_last<INV, N, ORD>(tw, tid, x, sv);
+      stage_r32_pair_last<INV, N>(tw, tid, x, sv);
     } else {
-      stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv, bar);
-      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R, ORD>(lds, tw, tid, ld, sv, bar);
+      stage_x<R, INV, N, L, T, IN_LDS, OUT_LDS, LIN, LOUT>(lds, tw, tid, ld, sv);
+      fft_pow2_io<INV, N, T, MODE, FIRST_LDS, LAST_LDS, S + 1, L * R>(lds, tw, tid, ld, sv);
     }
   }
 }

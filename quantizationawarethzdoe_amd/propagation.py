@@ -52,8 +52,13 @@ def asm_padding(H, W, padding_scale, do_padding=True):
 
 
 def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk=0,
-              mask=None):
-    """thz_asm_desc; ``mask``: an ApertureDesc on the output grid (thz_asm_desc.window_mask)."""
+              mask=None, z_dev=None):
+    """thz_asm_desc; ``mask``: an ApertureDesc on the output grid (thz_asm_desc.window_mask);
+    ``z_dev``: a float32 device tensor [Z] the kernels read the plane distances from
+    (thz_asm_desc.z_dev: graph-replayable planes; ``zs`` then only gives their count)."""
+    if z_dev is not None and (z_dev.dtype != torch.float32 or not z_dev.is_contiguous() or z_dev.numel() != len(zs)
+                              or z_dev.device.type != "cuda"):
+        raise ValueError(f"z_dev: a contiguous float32 device tensor of {len(zs)} planes")
     wl = _lib.float_array(wavelengths)
     zv = _lib.float_array(zs)
     d = _lib.AsmDesc(B=B, C=C, H=H, W=W, pad_h=pad_h, pad_w=pad_w, unpad=int(bool(unpad)),
@@ -61,8 +66,9 @@ def _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, 
                      dx=float(spacing[0]), dy=float(spacing[1]),
                      wavelengths=ctypes.cast(wl, ctypes.POINTER(ctypes.c_float)),
                      z=ctypes.cast(zv, ctypes.POINTER(ctypes.c_float)),
-                     window_mask=ctypes.addressof(mask) if mask is not None else None)
-    d._keep = (wl, zv, mask)
+                     window_mask=ctypes.addressof(mask) if mask is not None else None,
+                     z_dev=z_dev.data_ptr() if z_dev is not None else None)
+    d._keep = (wl, zv, mask, z_dev)
     return d
 
 
@@ -73,12 +79,22 @@ def window_mask_fusable(H, W, pad_h, pad_w, unpad, Z=1):
 
 
 def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint=False, z_chunk=0,
-              out=None, mask=None):
+              out=None, mask=None, z_dev=None):
     """Raw launch: forward data [B,C,H,W] -> [Z,B,C,Ho,Wo]; adjoint [Z,B,C,Ho,Wo] -> [B,C,H,W], the sum
     over the Z planes of each plane's adjoint (one pipeline: the column pass sums the planes'
     spectra, thz_asm_forward with adjoint = 1)."""
     _require_device(data, "ASM")
+    if mask is not None:
+        # the folded aperture exists in the complex64 300-point row passes only, and its adjoint takes
+        # one plane: refuse here, in the forward, rather than drop the mask or fail in backward
+        if data.dtype != torch.complex64:
+            raise TypeError(f"ASM window mask: complex64 fields only, got {data.dtype} (apply the aperture "
+                            "separately)")
+        if len(zs) != 1:
+            raise ValueError(f"ASM window mask: one z-plane per call, got {len(zs)}")
     if data.dtype == torch.complex128:
+        if z_dev is not None:
+            raise TypeError("ASM z_dev: complex64 fields only (the fp64 kernels take host planes)")
         return _asm64_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, adjoint, out)
     if data.dtype != torch.complex64:
         raise TypeError(f"ASM kernels compute in complex64 or complex128; got {data.dtype}")
@@ -95,7 +111,7 @@ def asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, ad
         B, C, H, W = data.shape
         Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
         out_shape = (len(zs), B, C, Ho, Wo)
-    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk, mask)
+    d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, adjoint, z_chunk, mask, z_dev)
     nbytes = ctypes.c_size_t(0)
     _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
     ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=data.device)
@@ -165,17 +181,19 @@ def asm_band_columns(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, sp
 
 class _AsmFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_chunk, mask):
-        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask)
-        return asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, False, z_chunk, mask=mask)
+    def forward(ctx, data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_chunk, mask, z_dev):
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev)
+        return asm_apply(data, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, False, z_chunk, mask=mask,
+                         z_dev=z_dev)
 
     @staticmethod
     def backward(ctx, g):
-        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask = ctx.cfg
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev = ctx.cfg
         # one adjoint launch for all planes: sum_z A_z^H g_z, the sum taken in the column pass (the
         # window mask, when folded, on the adjoint's input)
-        gin = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask)
-        return gin, None, None, None, None, None, None, None, None, None
+        gin = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask,
+                        z_dev=z_dev)
+        return gin, None, None, None, None, None, None, None, None, None, None
 
 
 def asm_transfer_function(wavelengths, spacing, z, H, W, pad_h, pad_w, bandlimit, device):
@@ -214,12 +232,13 @@ def rs_kernel(meshx, meshy, z, wavelengths):
 
 
 def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", z_chunk=0,
-                  mask=None):
+                  mask=None, z_dev=None):
     """Differentiable ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo] (HIP kernels); ``mask``: an
-    aperture folded onto the output (window_mask_fusable geometry only)."""
+    aperture folded onto the output (window_mask_fusable geometry only); ``z_dev``: the planes in
+    device memory (_asm_desc)."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
     return _AsmFunction.apply(data, list(map(float, wavelengths)), tuple(map(float, spacing)),
-                              list(map(float, zs)), int(pad_h), int(pad_w), bool(unpad), bl, int(z_chunk), mask)
+                              list(map(float, zs)), int(pad_h), int(pad_w), bool(unpad), bl, int(z_chunk), mask, z_dev)
 
 
 class _AsmModulatedFunction(torch.autograd.Function):
@@ -228,13 +247,14 @@ class _AsmModulatedFunction(torch.autograd.Function):
     (one launch), then the modulate backward kernel (grad_field, grad_height)."""
 
     @staticmethod
-    def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask):
+    def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev):
         _require_device(field, "ASM")
         field = field.contiguous()
         h = height.detach().contiguous().float()
         B, C, H, W = field.shape
         Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
-        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False, mask=mask)
+        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False, mask=mask,
+                      z_dev=z_dev)
         m = pend.desc()
         L = _lib.lib()
         nbytes = ctypes.c_size_t(0)
@@ -253,7 +273,7 @@ class _AsmModulatedFunction(torch.autograd.Function):
             pend.hfull = hfull
         ctx.save_for_backward(field, h)
         ctx.pend = pend
-        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask)
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev)
         return out
 
     @staticmethod
@@ -261,20 +281,22 @@ class _AsmModulatedFunction(torch.autograd.Function):
         from . import doe as _doe
         field, h = ctx.saved_tensors
         pend = ctx.pend
-        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask = ctx.cfg
-        gm = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask)
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev = ctx.cfg
+        gm = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask,
+                       z_dev=z_dev)
         gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
                                         ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
-        return gf, gh, None, None, None, None, None, None, None, None, None
+        return gf, gh, None, None, None, None, None, None, None, None, None, None
 
 
-def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", mask=None):
+def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", mask=None,
+                            z_dev=None):
     """Differentiable fused DOE modulation + ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo]; ``mask``
-    as asm_propagate."""
+    and ``z_dev`` as asm_propagate."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
     return _AsmModulatedFunction.apply(pend.field, pend.height, pend, list(map(float, wavelengths)),
                                        tuple(map(float, spacing)), list(map(float, zs)), int(pad_h), int(pad_w),
-                                       bool(unpad), bl, mask)
+                                       bool(unpad), bl, mask, z_dev)
 
 
 class _AsmLossFunction(torch.autograd.Function):

@@ -112,9 +112,153 @@ class FourFocalSpotsSystem(nn.Module):
         return self.asm_prop3(self.doe(self.input_field, iter_frac))
 
 
+# ---------------------------------------------------------------------------------------------
+# The reference's two multi-plane QAT systems (plot_data/example_2 and example_3): one DOE, several
+# output planes, loss = sum over the planes of MSE(normalize(|E_z|^2), target_z).
+# ---------------------------------------------------------------------------------------------
+def dual_plane_params():
+    """doe_params / optim_params of experiment_dual_plane_hologram.ipynb cell 2 (high-temp resin:
+    tan d 0.003, 50 um tolerance, no unit-cell mirroring)."""
+    doe_params = {
+        'doe_size': [100, 100], 'doe_dxy': 1 * mm, 'doe_level': 4, 'look_up_table': None, 'num_unit': None,
+        'height_constraint_max': 1 * mm, 'tolerance': 0.05 * mm, 'material': [2.66, 0.003],
+    }
+    return doe_params, {'c_s': 100, 'tau_max': 2.5, 'tau_min': 1.5}
+
+
+def edof_params():
+    """doe_params / optim_params of experiment_extend_depth_of_focus.ipynb cell 1 (the second,
+    effective optim_params of the cell)."""
+    doe_params = {
+        'doe_size': [100, 100], 'doe_dxy': 1 * mm, 'doe_level': 4, 'look_up_table': None, 'num_unit': None,
+        'height_constraint_max': 1 * mm, 'tolerance': 10 * um, 'material': [2.66, 0.03],
+    }
+    return doe_params, {'c_s': 100, 'tau_max': 2.5, 'tau_min': 1.5}
+
+
+def logo_targets(device=None):
+    """The dual-plane notebook's two targets (cells 3-4: the Aalto logos, grayscale, normalised,
+    zero-padded 140 / 90 and nearest-resized from round(.) to 100 x 100) as [2, 1, 100, 100].  The
+    PNGs are decoded in the build container by tests/golden/gen_qat_multi.py, which writes the
+    resulting 0 / 1 maps to data/dual_plane_targets.npz; nothing here needs the image files."""
+    import os
+    import numpy as np
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "dual_plane_targets.npz")
+    with np.load(path, allow_pickle=False) as z:
+        t = torch.from_numpy(z["targets"].astype(np.float32))
+    return t[:, None].to(device or torch.device("cuda"))
+
+
+def edof_target(wavelength=C0 / 300e9, device=None):
+    """The extended-DOF notebook's target (cells 2-3): define_FoM at f = 100 mm on the axis."""
+    return define_FoM([100, 100], 1 * mm, wavelength, 100 * mm, [0 * mm, 0 * mm], device=device)
+
+
+class MultiPlaneSystem(nn.Module):
+    """Submm_Setupv2 of the multi-plane notebooks: Gaussian source (BeamWaistCorruagtedTK waist) ->
+    ASM 127 mm -> lens f = 127 mm [-> ASM 127 mm, ``second_prop``] -> 80 mm square aperture -> DOE ->
+    one ASM_prop per output plane, all with the same padding and the exact band limit.
+
+    ``forward(iter_frac)`` is the notebook's: a list of ElectricFields, one per plane.
+    ``forward_planes(iter_frac)`` is the MI355X path the trainer uses: every plane from ONE
+    pipeline (the DOE modulation fused into the shared row pass, one column pass over the Z planes,
+    and in backward the Z-summing adjoint: one launch for all planes), [Z, B, C, H, W]."""
+
+    def __init__(self, planes_m, padding_scale, doe_class, doe_params, optim_params, input_dxy=1 * mm,
+                 input_field_shape=(100, 100), wavelengths=C0 / 300e9, second_prop=False, device=None):
+        super().__init__()
+        self.doe_params, self.optim_params = doe_params, optim_params
+        self.device = device or torch.device("cuda")
+        self.wavelengths = wavelengths
+        self.second_prop = second_prop
+        kw = dict(bandlimit_type='exact', padding_scale=padding_scale, bandlimit_kernel=True, device=self.device)
+        self.source = Guassian_beam(height=input_field_shape[0], width=input_field_shape[1], beam_waist_x=None,
+                                    beam_waist_y=None, wavelengths=wavelengths, spacing=input_dxy, device=self.device)
+        self.asm_prop1 = ASM_prop(z_distance=0.127 * m, **kw)
+        self.Colli_lens = Thin_LensElement(focal_length=0.127 * m)
+        if second_prop:
+            self.asm_prop2 = ASM_prop(z_distance=0.127 * m, **kw)
+        self.aperture = ApertureElement(aperture_type='rect', aperture_size=0.08)
+        with torch.no_grad():
+            self.input_field = self.field_before_DOE()
+        if doe_class.__name__.endswith("FullPrecisionDOELayer"):
+            self.doe = doe_class(self.doe_params, device=self.device)
+        else:
+            self.doe = doe_class(self.doe_params, self.optim_params, device=self.device)
+        self.props = nn.ModuleList([ASM_prop(z_distance=z, **kw) for z in planes_m])
+
+    def field_before_DOE(self):
+        field = self.asm_prop1(self.source())
+        field = self.Colli_lens(field)
+        if self.second_prop:
+            field = self.asm_prop2(field)
+        return self.aperture(field)
+
+    @property
+    def planes(self):
+        """The current plane distances (m), host floats."""
+        return [float(p._zh[0]) for p in self.props]
+
+    def forward(self, iter_frac):
+        field = self.doe(self.input_field, iter_frac)
+        return [p(field) for p in self.props]
+
+    def forward_planes(self, iter_frac, z_dev=None):
+        """[Z, B, C, H, W]; ``z_dev``: the planes read from device memory (graph replay)."""
+        field = self.doe(self.input_field, iter_frac)
+        return self.props[0].propagate_planes(field, self.planes, z_dev=z_dev)
+
+    def after_forward(self):
+        """Per-iteration plane update of the notebook's forward (none here; ExtendedDOFSystem)."""
+
+
+class DualPlaneSystem(MultiPlaneSystem):
+    """experiment_dual_plane_hologram.ipynb cell 6 ("Ours"): padding 2, planes 100 and 150 mm, the
+    score-Gumbel v3 layer; the full-precision / naive-Gumbel / PSQ / STE cells (16, 39, 46, 53) add
+    the second 127 mm propagation before the aperture (``second_prop``)."""
+
+    def __init__(self, doe_class=Q.SoftGumbelQuantizedDOELayerv3, doe_params=None, optim_params=None,
+                 second_prop=None, device=None):
+        dp, op = dual_plane_params()
+        if second_prop is None:
+            second_prop = doe_class is not Q.SoftGumbelQuantizedDOELayerv3
+        super().__init__([100 * mm, 150 * mm], 2, doe_class, doe_params or dp, optim_params or op,
+                         second_prop=second_prop, device=device)
+
+
+class ExtendedDOFSystem(MultiPlaneSystem):
+    """experiment_extend_depth_of_focus.ipynb cell 22 ("Ours"): padding 4 (P = 500), the rotationally
+    symmetric score-Gumbel layer, planes at 50 / 60 / 70 / 80 / 90 mm re-drawn after every forward
+    (50 + U(0, 5), 60 + U(-5, 5), 70 + U(-5, 5), 80 + U(-5, 5), 90 + U(-5, 0) mm; the notebook uses
+    python's unseeded random.uniform, here a random.Random(seed)).  The full-precision cell (6) adds
+    the second 127 mm propagation."""
+    JITTER_MM = [(50, 0, 5), (60, -5, 5), (70, -5, 5), (80, -5, 5), (90, -5, 0)]
+
+    def __init__(self, doe_class=Q.RotationallySymmetricScoreGumbelSoftQuantizedDOELayer, doe_params=None,
+                 optim_params=None, second_prop=None, seed=0, device=None):
+        import random
+        dp, op = edof_params()
+        if second_prop is None:
+            second_prop = doe_class is Q.RotationallySymmetricFullPrecisionDOELayer
+        super().__init__([c * mm for c, _, _ in self.JITTER_MM], 4, doe_class, doe_params or dp, optim_params or op,
+                         second_prop=second_prop, device=device)
+        self.rand = random.Random(seed)
+
+    def forward(self, iter_frac):
+        outs = super().forward(iter_frac)
+        self.after_forward()
+        return outs
+
+    def after_forward(self):
+        for p, (c, lo, hi) in zip(self.props, self.JITTER_MM):
+            p.z = c * mm + self.rand.uniform(lo * mm, hi * mm)
+
+
 class StepState:
-    """The per-step device state of a graph-replayed trainer: int32 [5] = the float32 bits of the
-    layer schedule (tau, s, beta), then the device generator's (seed, step).
+    """The per-step device state of a graph-replayed trainer: int32 [5 + nz] = the float32 bits of
+    the layer schedule (tau, s, beta), the device generator's (seed, step), then the float32 bits of
+    the nz output-plane distances of a multi-plane system (``zdev``: the ASM kernels read them,
+    thz_asm_desc.z_dev, so the extended-DOF planes can move every replay).
 
     ``upload`` writes the host values into one slot of a pinned ring and enqueues an asynchronous
     copy into the device state on the current stream: no pageable (synchronous) host->device copy
@@ -126,19 +270,20 @@ class StepState:
     pointers, while eager forwards after training draw from torch's generator and use their own
     iter_frac, as the reference's layers do."""
 
-    def __init__(self, device, seed, device_rng, depth=8):
+    def __init__(self, device, seed, device_rng, depth=8, nz=0):
         import numpy as np
-        self.state = torch.zeros(5, dtype=torch.int32, device=device)
+        self.state = torch.zeros(5 + nz, dtype=torch.int32, device=device)
         self.dyn = self.state[:3].view(torch.float32)
+        self.zdev = self.state[5:].view(torch.float32) if nz else None
         self.seed = seed
         self.device_rng = device_rng
-        self._pinned = torch.zeros(depth, 5, dtype=torch.int32).pin_memory()
+        self._pinned = torch.zeros(depth, 5 + nz, dtype=torch.int32).pin_memory()
         self._host = self._pinned.numpy()
         self._np = np
         self._events = [None] * depth
         self._k = 0
 
-    def upload(self, dyn, step):
+    def upload(self, dyn, step, zs=None):
         k = self._k
         self._k = (k + 1) % len(self._events)
         ev = self._events[k]
@@ -149,6 +294,8 @@ class StepState:
         self._host[k, :3] = self._np.asarray(dyn, dtype=self._np.float32).view(self._np.int32)
         self._host[k, 3] = int(self.seed)
         self._host[k, 4] = int(step) & 0x7FFFFFFF
+        if zs is not None:
+            self._host[k, 5:] = self._np.asarray(zs, dtype=self._np.float32).view(self._np.int32)
         self.state.copy_(self._pinned[k], non_blocking=True)
         ev.record()
 
@@ -304,6 +451,16 @@ class QATTrainer:
                  device_rng=True, capture_collective=False, force_collective=False, optimizer="adam"):
         self.system = system
         self.target = target.to(system.device).float().contiguous()
+        # multi-plane systems (MultiPlaneSystem): ``target`` is [Z, 1, H, W] (one per plane) or
+        # [1, 1, H, W] (shared); the loss kernel sees the planes as its batch
+        self.multi = hasattr(system, "forward_planes")
+        self._zs_graph = None
+        if self.multi:
+            Z, B = len(system.planes), system.input_field.shape[0]
+            t = self.target.reshape((-1, 1) + tuple(self.target.shape[-2:]))
+            if t.shape[0] not in (1, Z):
+                raise ValueError(f"multi-plane target: {t.shape[0]} maps for {Z} planes")
+            self.target = (t.repeat_interleave(B, 0) if t.shape[0] == Z and B > 1 else t).contiguous()
         self.max_itrs = max_itrs
         self.graph = graph
         # loss(out_field_data, target): the fused HIP |E|^2 -> normalize -> MSE by default
@@ -324,8 +481,10 @@ class QATTrainer:
             # with device_rng the layer's Gumbel and height-noise draws are made in the kernels from
             # it (no torch RNG kernels, nor their per-replay offset fills, in the captured graph)
             seed = int(torch.randint(0, 2 ** 31 - 1, (1,)).item()) if device_rng else 0
-            self._step_state = StepState(system.device, seed, device_rng)
+            self._step_state = StepState(system.device, seed, device_rng, nz=len(system.planes) if self.multi else 0)
             self.dyn = self._step_state.dyn
+            # multi-plane: the captured propagation reads its planes from the step state
+            self._zs_graph = self._step_state.zdev
 
     def _frac(self, iter_frac):
         return self.itr / self.max_itrs if iter_frac is None else iter_frac
@@ -333,7 +492,16 @@ class QATTrainer:
     # The step in two phases around the one collective; the eager step and the captured graphs
     # run the same two functions (fwd/bwd + pack | all-reduce | unpack + Adam).
     def _fb(self, frac):
-        if self.loss_fn is _optics.intensity_mse:
+        if self.multi:
+            # every plane from one pipeline ([Z, B, C, H, W]; backward: the Z-summing adjoint), the
+            # loss kernel over the Z B planes as its batch (normalize is per plane), x Z: the sum
+            # over the planes of each plane's mean
+            out = self.system.forward_planes(frac, z_dev=self._zs_graph)
+            if self._zs_graph is None:
+                self.system.after_forward()  # the notebook's per-iteration plane update (eager)
+            Z, B = out.shape[:2]
+            loss = _optics.intensity_mse(out.reshape((Z * B,) + tuple(out.shape[2:])), self.target) * float(Z)
+        elif self.loss_fn is _optics.intensity_mse:
             # the default loss folded into the last propagation
             with _prop.deferred_output():
                 out = self.system(frac)
@@ -422,7 +590,8 @@ class QATTrainer:
 
     def _graph_step(self, frac):
         phase = self.system.doe._graph_phase(frac)
-        self._step_state.upload(self.system.doe._dyn_values(frac), self.itr)
+        self._step_state.upload(self.system.doe._dyn_values(frac), self.itr,
+                                self.system.planes if self.multi else None)
         if phase not in self._graphs:
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
@@ -430,6 +599,8 @@ class QATTrainer:
         if g_opt is not None:  # an eager collective between the two captured halves
             self.allreduce.reduce()
             g_opt.replay()
+        if self.multi:
+            self.system.after_forward()  # the next replay's planes (the notebook's per-iteration update)
         return loss
 
     def train(self, steps, log_every=200, log=print):

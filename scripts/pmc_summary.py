@@ -47,10 +47,9 @@ def main():
     import datetime
     traffic = {"_meta": {"profile": f"profiles/{tag}_pmc_summary.json", "date": datetime.date.today().isoformat(),
                          "note": "per-launch HBM bytes of the bench's cfg2 kernels, keyed by bench.py's timer names"}}
-    # kernel name -> the KernelTimer name bench.py reports it under (the four-step / paired /
-    # middle-crop column passes are timed as asm_cols, the middle-crop row pass as asm_rows_inv)
-    alias = {"asm_cols_4s": "asm_cols", "asm_cols_4s_pair": "asm_cols", "asm_cols_pair": "asm_cols",
-             "asm_cols_mid": "asm_cols", "asm_rows_inv_mid": "asm_rows_inv", "asm_rows_inv_4s": "asm_rows_inv"}
+    # kernel name -> the KernelTimer name bench.py reports it under (the middle-crop row pass is
+    # timed as asm_rows_inv)
+    alias = {"asm_rows_inv_mid": "asm_rows_inv"}
     for k, d in summ.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             b = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0

@@ -51,6 +51,14 @@ int main(void) {
   EXPECT(thz_asm_forward(&a, NULL, NULL, NULL, 0, NULL) != THZ_OK, "asm forward null data");
   char dummy[64];
   EXPECT(thz_asm_forward(&a, dummy, dummy, dummy, 8, NULL) == THZ_E_WORKSPACE, "asm workspace too small");
+  /* ABI 6: device-resident planes (z_dev) need no host z; the band is then sized for any z */
+  b = a; b.z = NULL; b.z_dev = (const float*)dummy;
+  int ncols_dev = 0, zc_dev = 0;
+  EXPECT(thz_asm_band(&b, &ncols_dev, &zc_dev) == THZ_OK && ncols_dev >= ncols && zc_dev == zc, "asm z_dev band");
+  b = a; b.z = NULL;
+  EXPECT(thz_asm_workspace_size(&b, &ws) == THZ_E_ARG, "asm without host or device z");
+  b = a; b.z = NULL; b.z_dev = (const float*)dummy;
+  EXPECT(thz_asm_transfer_function(&b, dummy, NULL) == THZ_E_ARG, "transfer function needs a host z");
   /* inspection entries: rejections before any launch */
   EXPECT(thz_asm_transfer_function(NULL, dummy, NULL) != THZ_OK, "transfer function null descriptor");
   EXPECT(thz_asm_transfer_function(&a, NULL, NULL) == THZ_E_ARG, "transfer function null output");

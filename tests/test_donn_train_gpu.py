@@ -115,57 +115,56 @@ def test_donn_step_b256_vs_reference_step(chained):
     assert chk["ok"], chk
 
 
-_FOLD_SCRIPT = r"""
-import sys, torch
-sys.path.insert(0, {root!r})
-from quantizationawarethzdoe_amd import donn, propagation
-from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
-from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
-from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
-from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
-assert propagation.window_mask_fusable(100, 100, 100, 100, True)  # the fold is what runs
-dev = torch.device("cuda:0")
-for kind, size in (("rect", 0.08), ("circ", 0.03)):
-    for modulated in (False, True):
-        g = torch.Generator(device=dev).manual_seed(4)
-        x = torch.randn(3, 1, 100, 100, dtype=torch.complex64, device=dev, generator=g)
-        cot = torch.randn(3, 1, 100, 100, dtype=torch.complex64, device=dev, generator=g)
-        prop = ASM_prop(z_distance=0.02, padding_scale=2, bandlimit_type="exact", device=dev)
-        res = []
-        for fused in (True, False):
-            torch.manual_seed(11)
-            xi = x.clone().requires_grad_(True)
-            f = ElectricField(data=xi, wavelengths=2.998e8 / 300e9, spacing=1e-3, device=dev)
-            doe = None
-            if modulated:
-                dp, _ = donn.default_params()
-                doe = Q.FullPrecisionDOELayer(dict(dp, tolerance=0.0), device=dev)
-                f = doe(f, 0.5)
-            ap = ApertureElement(aperture_type=kind, aperture_size=size)
-            out = donn.propagate_through_aperture(prop, ap, f) if fused else ap(prop(f))
-            out.data.backward(cot)
-            gw = next(iter(doe.parameters())).grad.clone() if doe is not None else None
-            res.append((out.data.detach().clone(), xi.grad.clone(), gw, ap.aperture.clone()))
-        (o1, g1, w1, m1), (o2, g2, w2, m2) = res
-        assert torch.equal(o1, o2) and torch.equal(g1, g2) and torch.equal(m1, m2), (kind, modulated)
-        if modulated:
-            assert torch.equal(w1, w2), (kind, modulated)
-print("ok")
-"""
-
-
 def test_aperture_folded_into_asm_matches_the_modules():
     """donn.propagate_through_aperture (the aperture as thz_asm_desc.window_mask: the 300-point row
     pass multiplies its stores by the mask, the backward's row pass its loads) == ApertureElement
     after ASM_prop, rect and circ, for a plain field and for a DOE layer's unevaluated modulation:
     the same values bit for bit (v or v * 0), forward and gradients, and the same .aperture
-    attribute.  Both row-pass forms: the default 5 3 4 5 kernels and the opt-in 3 x 100 split
-    (THZ_K2_M3=1), each in a child process (the switch is read once per process)."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    for flag in ("0", "1"):
-        r = subprocess.run([sys.executable, "-c", _FOLD_SCRIPT.format(root=root)], env=dict(os.environ, THZ_K2_M3=flag),
-                           cwd=root, capture_output=True, text=True, timeout=240)
-        assert r.returncode == 0 and "ok" in r.stdout, (flag, r.stderr[-2000:])
+    attribute."""
+    from quantizationawarethzdoe_amd import donn, propagation
+    from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+    from quantizationawarethzdoe_amd.Components.Aperture import ApertureElement
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    assert propagation.window_mask_fusable(100, 100, 100, 100, True)  # the fold is what runs
+    dev = _dev()
+    for kind, size in (("rect", 0.08), ("circ", 0.03)):
+        for modulated in (False, True):
+            g = torch.Generator(device=dev).manual_seed(4)
+            x = torch.randn(3, 1, 100, 100, dtype=torch.complex64, device=dev, generator=g)
+            cot = torch.randn(3, 1, 100, 100, dtype=torch.complex64, device=dev, generator=g)
+            prop = ASM_prop(z_distance=0.02, padding_scale=2, bandlimit_type="exact", device=dev)
+            res = []
+            for fused in (True, False):
+                torch.manual_seed(11)
+                xi = x.clone().requires_grad_(True)
+                f = ElectricField(data=xi, wavelengths=2.998e8 / 300e9, spacing=1e-3, device=dev)
+                doe = None
+                if modulated:
+                    dp, _ = donn.default_params()
+                    doe = Q.FullPrecisionDOELayer(dict(dp, tolerance=0.0), device=dev)
+                    f = doe(f, 0.5)
+                ap = ApertureElement(aperture_type=kind, aperture_size=size)
+                out = donn.propagate_through_aperture(prop, ap, f) if fused else ap(prop(f))
+                out.data.backward(cot)
+                gw = next(iter(doe.parameters())).grad.clone() if doe is not None else None
+                res.append((out.data.detach().clone(), xi.grad.clone(), gw, ap.aperture.clone()))
+            (o1, g1, w1, m1), (o2, g2, w2, m2) = res
+            assert torch.equal(o1, o2) and torch.equal(g1, g2) and torch.equal(m1, m2), (kind, modulated)
+            if modulated:
+                assert torch.equal(w1, w2), (kind, modulated)
+
+
+def test_window_mask_refused_for_complex128_and_several_planes():
+    """The folded aperture exists in the complex64 one-plane pipeline only: asm_apply refuses a mask
+    with a complex128 field or more than one z-plane in the forward, instead of dropping
+    it or failing in the backward."""
+    from quantizationawarethzdoe_amd import _lib, propagation
+    dev = _dev()
+    m = _lib.ApertureDesc(1, 100, 100, _lib.APERTURE_RECT, 1e-3, 1e-3, 0.04, 0.04, 0.0)
+    x = torch.randn(1, 1, 100, 100, dtype=torch.complex64, device=dev)
+    lam = [2.998e8 / 300e9]
+    with pytest.raises(TypeError):
+        propagation.asm_apply(x.to(torch.complex128), lam, [1e-3, 1e-3], [0.02], 100, 100, True, 1, mask=m)
+    with pytest.raises(ValueError):
+        propagation.asm_apply(x, lam, [1e-3, 1e-3], [0.02, 0.03], 100, 100, True, 1, mask=m)

@@ -10,7 +10,8 @@ is on robust statistics: the median over seeds of the mean of the last 100 itera
 [0.5x, 2x] of the reference curve's, the median minimum within [0.5x, 2x] of the reference's
 minimum, and the loss at iterations 200 / 400 within [0.5x, 2x] of the span of the two reference
 runs (the saved curve and the printed trace differ by up to 1.5x there).  scripts/qat_quality.py
-runs every method of the notebook with five seeds (profiles/r04_qat_quality.json)."""
+runs every method of the notebook with five seeds (profiles/r04_qat_quality.json), and with
+--system dual / edof the methods of the dual-plane and extended-DOF notebooks (profiles/r05_*)."""
 import json
 import os
 
@@ -65,6 +66,41 @@ def test_naive_gumbel_six_thousand_iterations_stay_finite_and_within_the_envelop
     runs = []
     for seed in range(3):
         curve, _ = run_method("GS", seed)
+        assert np.all(np.isfinite(curve)), seed
+        runs.append(stats(curve))
+    last100 = float(np.median([s["mean_last100"] for s in runs]))
+    mn = float(np.median([s["min"] for s in runs]))
+    assert 0.5 * r["mean_last100"] <= last100 <= 2.0 * r["mean_last100"], (last100, r["mean_last100"])
+    assert 0.5 * r["min"] <= mn <= 2.0 * r["min"], (mn, r["min"])
+
+
+ENVELOPE_CASES = [
+    # (system, method): example_1's remaining methods and the "Ours" runs of
+    # the two multi-plane systems (item 2)
+    ("four_focal", "STE"), ("four_focal", "PSQ"), ("four_focal", "full"),
+    ("dual", "Ours"), ("edof", "Ours"),
+]
+
+
+@pytest.mark.parametrize("system,method", ENVELOPE_CASES, ids=[f"{s}-{m}" for s, m in ENVELOPE_CASES])
+def test_six_thousand_iterations_within_the_reference_envelope(system, method):
+    """The notebook's whole 6,000-iteration run of one method of one system (scripts/qat_quality.py:
+    the layer, optim_params, optimiser and lr of its cell), three seeds on the graph-replayed
+    trainer: every loss finite, the median over seeds of the mean of the last 100 iterations and of
+    the minimum within [0.5x, 2x] of the reference's own curve (plot_data/example_1, _2 or _3
+    loss_curve_<method>.npy via tests/golden/qat_curves.json).  The multi-plane systems propagate
+    their planes in one pipeline with the Z-summing adjoint; the extended-DOF planes move every
+    iteration (read from the device step state) and its P = 500 transforms run the runtime
+    mixed-radix plan."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
+    from qat_quality import reference, run_method, stats
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    r = reference(system, method)
+    runs = []
+    for seed in range(3):
+        curve, _ = run_method(method, seed, system=system)
         assert np.all(np.isfinite(curve)), seed
         runs.append(stats(curve))
     last100 = float(np.median([s["mean_last100"] for s in runs]))
