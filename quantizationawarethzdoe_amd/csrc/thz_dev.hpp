@@ -28,33 +28,28 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 // touches one 8-B element per segment; the CB column workgroups sharing a segment run on
 // one XCD back to back (xcd_chunk) so the L2 merges their partial lines.
 //
-// The per-z intermediate U (column pass -> row pass) uses narrower blocks, CBU = 4 columns =
-// one 32-B sector: the column pass then fills whole sectors from 4 co-scheduled workgroups
-// (the L2 writes back partially dirty sectors at a cost: measured K2 1.93 ms at 16 columns,
-// 1.69 at 8, 1.39 at 4, 1.33 unblocked), while the row pass still gathers whole sectors
-// (K3 1.05 ms at 16, 1.22 at 4, 2.59 unblocked).  cfg2 sum per z-chunk is lowest at 4.
+// The per-z intermediate U (column pass -> row pass) uses narrower blocks, CBU = 4 columns (the
+// L2 writes back partially dirty sectors at a cost: measured K2 1.93 ms at 16 columns, 1.69 at
+// 8, 1.39 at 4, 1.33 unblocked, while the row pass gathers K3 1.05 ms at 16, 1.22 at 4, 2.59
+// unblocked; cfg2 sum per z-chunk lowest at 4), laid out as below.
 constexpr int CB = 16;
 constexpr int CBU = 4;
 __device__ __forceinline__ size_t blk(int c, int row, int rows) {
   return ((size_t)(c / CB) * rows + row) * CB + (c % CB);
 }
-#ifndef THZ_UL
-#define THZ_UL 0
-#endif
-// THZ_UL = 1 (A/B build): U in 4 x 4 tiles of (column, row) whose 32-B sectors are 4 consecutive ROWS
-// of one column -- the 128-B line holds the same 16 elements as the blocked layout, transposed --
-// so the column pass writes whole sectors itself and the row pass reads 8 B of each of 4 sectors.
-// U's rows are padded to a multiple of 4 (u_rows).
-__host__ __device__ constexpr int u_rows(int rows) { return THZ_UL ? (rows + 3) & ~3 : rows; }
+// U (the column pass's output, the inverse row pass's input) in 4 x 4 tiles of (column, row): a
+// 32-B sector holds 4 consecutive ROWS of one column, so each store instruction of the column pass
+// fills whole sectors itself (rows j..j+3 of one column come from one workgroup), and the row pass reads
+// 8 B of each of 4 sectors of a 128-B line.  The row-major CBU-column blocking it replaced had its
+// 32-B sectors written by the 4 column workgroups of a block: 1.65x U in WRITE_SIZE and K2 4.39 ->
+// 4.17 ms at cfg2 on the same box (profiles/r05_experiments.txt).  U's rows are padded to a
+// multiple of 4 (u_rows).
+__host__ __device__ constexpr int u_rows(int rows) { return (rows + 3) & ~3; }
 __device__ __forceinline__ size_t blk_u(int c, int row, int rows) {
-  if constexpr (THZ_UL) return ((size_t)(c / CBU) * u_rows(rows) + (row & ~3)) * CBU + (c % CBU) * 4 + (row & 3);
-  return ((size_t)(c / CBU) * rows + row) * CBU + (c % CBU);
+  return ((size_t)(c / CBU) * u_rows(rows) + (row & ~3)) * CBU + (c % CBU) * 4 + (row & 3);
 }
 // offset of row r from row 0 of the same column of U
-__device__ __forceinline__ size_t u_roff(int r) {
-  if constexpr (THZ_UL) return (size_t)(r & ~3) * CBU + (r & 3);
-  return (size_t)r * CBU;
-}
+__device__ __forceinline__ size_t u_roff(int r) { return (size_t)(r & ~3) * CBU + (r & 3); }
 
 
 // sin/cos of a float angle (|ang| up to ~1e5 rad): 3-constant Cody-Waite reduction by pi/2
