@@ -51,13 +51,14 @@ typedef void* thz_stream_t; /* hipStream_t */
 
 /* ABI of this header.  Bumped whenever a descriptor struct changes layout (round 2 appended
  * rng / rng_stream to thz_doe_desc and thz_quant_desc; 4 added thz_asm_transfer_function and
- * thz_rs_kernel, which the bindings require; 5 appended thz_asm_desc.window_mask, 6 thz_asm_desc.z_dev):
+ * thz_rs_kernel, which the bindings require; 5 appended thz_asm_desc.window_mask, 6 thz_asm_desc.z_dev,
+ * 7 added thz_doe_quant_backward):
  * a caller compares thz_abi_version()
  * with the THZ_ABI_VERSION it was compiled against before its first call, since a shorter
  * struct from an older header would make the library read past it.  Descriptors are plain C
  * structs: zero-initialise them (memset / `= {0}` / ctypes defaults) so fields a caller does not
  * know about stay 0 (no noise buffer and no device generator means no noise). */
-#define THZ_ABI_VERSION 6
+#define THZ_ABI_VERSION 7
 
 /* Library identity. */
 const char* thz_version(void);
@@ -261,6 +262,19 @@ int thz_quant_forward(const thz_quant_desc* d, const float* weight, const float*
                       float* y_soft, thz_stream_t stream);
 int thz_quant_backward(const thz_quant_desc* d, const float* weight, const float* y_soft, const float* grad_full,
                        float* grad_weight, thz_stream_t stream);
+
+/*
+ * The whole backward of a quantized DOE layer whose height map has the field's size (no nearest
+ * upsampling): thz_doe_modulate_backward followed by thz_quant_backward in ONE kernel, the height
+ * gradient never written (DOELayer.modulate :92-126 and the quantizer's backward, e.g. v3
+ * :794-860).  d: the modulation (hs == H, ws == W); q: the quantizer that produced `height`
+ * (its full map, mirrored or not, must be [H, W]).  grad_field (NULL to skip) as
+ * thz_doe_modulate_backward, grad_weight as thz_quant_backward; bit-identical to the two calls.
+ * THZ_E_UNSUPPORTED for an upsampled map (use the two calls).
+ */
+int thz_doe_quant_backward(const thz_doe_desc* d, const thz_quant_desc* q, const void* grad_out, const void* field,
+                           const float* height, const float* noise, const float* weight, const float* y_soft,
+                           void* grad_field, float* grad_weight, thz_stream_t stream);
 
 /*
  * Radial profile -> 2-D height map of the rotationally symmetric layers

@@ -106,13 +106,14 @@ class DOELayer(nn.Module):
         ASM_prop forms it inside its row pass (one pipeline), any other reader of
         ``.data`` forms it with the modulate kernel."""
         h = preprocessed_height_map
+        link = getattr(h, "_thz_quant", None)  # the quantizer that made h (doe.QuantLink), if any
         if h.dim() != 2:
             h = h.reshape(h.shape[-2:])
         tol = None if height_tolerance is None else self._host_scalar("tol", height_tolerance)
         data = input_field.data
         self._pending_mod = _doe.PendingModulation(data, h, input_field.wavelengths_host,
                                                    self._host_scalar("eps", epsilon), self._host_scalar("tand", tand),
-                                                   tolerance=tol, rng=self._rng_spec(0))
+                                                   tolerance=tol, rng=self._rng_spec(0), quant=link)
         out = ElectricField(data=data, wavelengths=input_field.wavelengths,
                             spacing=input_field.spacing)._adopt_host(input_field)
         out._pending = self._pending_mod

@@ -305,15 +305,11 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
   for_mirrors(a, i, j, [&](int o) { hfull[o] = out; });
 }
 
-__global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __restrict__ ysave,
-                          const float* __restrict__ gfull, float* __restrict__ gw) {
-  const QDyn q = get_dyn(a);
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = a.hq * a.wq;
-  if (p >= n) return;
-  const int i = p / a.wq, j = p - i * a.wq;
-  float G = 0.f;
-  for_mirrors(a, i, j, [&](int o) { G += gfull[o]; });
+// dL/dw of quadrant pixel p from G = dL/dh summed over its mirror positions (the chain of
+// quant_fwd's pixel, reversed); NGS writes its L logits' gradients
+__device__ __forceinline__ void quant_bwd_px(const QArgs& a, const QDyn& q, const float* __restrict__ w,
+                                             const float* __restrict__ ysave, int p, int n, float G,
+                                             float* __restrict__ gw) {
   if (a.kind == THZ_Q_NGS) {
     // d logits_l = y_l (dy_l - sum_k y_k dy_k) / tau, dy_l = G lut_l
     float dot = 0.f;
@@ -369,6 +365,77 @@ __global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __r
   }
   const bool inside = wv >= -a.clampv && wv <= a.clampv;  // clamp passes the gradient on [min, max]
   gw[p] = inside ? dhm * a.hmax * sg * (1.0f - sg) : 0.0f;
+}
+
+__global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __restrict__ ysave,
+                          const float* __restrict__ gfull, float* __restrict__ gw) {
+  const QDyn q = get_dyn(a);
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.hq * a.wq;
+  if (p >= n) return;
+  const int i = p / a.wq, j = p - i * a.wq;
+  float G = 0.f;
+  for_mirrors(a, i, j, [&](int o) { G += gfull[o]; });
+  quant_bwd_px(a, q, w, ysave, p, n, G, gw);
+}
+
+// The DOE layer's whole backward in one pass, for a height map of the field's own size (no
+// upsampling): modulate backward (grad_field = g conj(t) for every (b, c); dL/dh per full-map
+// pixel, the batch summed over a.bl lanes in LDS exactly as doe_modulate_bwd does) and the
+// quantizer's backward of the quadrant pixel those full-map pixels mirror (for_mirrors order), so
+// grad_height never goes to memory.  Block = MOD_THREADS threads = (MOD_THREADS / a.bl) quadrant
+// pixels x a.bl batch lanes; results bit-identical to doe_modulate_bwd followed by quant_bwd.
+__global__ void __launch_bounds__(MOD_THREADS) doe_modulate_quant_bwd(const float2* __restrict__ g,
+                                                                      const float2* __restrict__ f,
+                                                                      const float* __restrict__ h,
+                                                                      const float* __restrict__ u,
+                                                                      float2* __restrict__ gf, ModArgs a, QArgs qa,
+                                                                      const float* __restrict__ w,
+                                                                      const float* __restrict__ ysave,
+                                                                      float* __restrict__ gw) {
+  __shared__ float red[MOD_THREADS];
+  const int HW = a.H * a.W;
+  const int n = qa.hq * qa.wq;
+  const int PX = MOD_THREADS / a.bl;
+  const int px = threadIdx.x % PX, lane = threadIdx.x / PX;
+  const int p = blockIdx.x * PX + px;
+  const bool live = p < n;
+  const int i = live ? p / qa.wq : 0, j = live ? p - i * qa.wq : 0;
+  int pos[4];
+  int nm = 0;
+  for_mirrors(qa, i, j, [&](int o) { pos[nm++] = o; });
+  float G = 0.f;
+  for (int k = 0; k < nm; ++k) {
+    float acc = 0.f;
+    if (live) {
+      const int o = pos[k];
+      const float hv = noisy_h(h, u, o, a);
+      for (int c = 0; c < a.C; ++c) {
+        float2 gam;
+        const float2 t = transmission(hv, a.lam[c], a, &gam);
+        float2 gt = make_float2(0.f, 0.f);  // sum_b g conj(f), this lane's share
+        for (int b = lane; b < a.B; b += a.bl) {
+          const size_t e = ((size_t)b * a.C + c) * HW + o;
+          const float2 gv = g[e];
+          if (gf) gf[e] = make_float2(gv.x * t.x + gv.y * t.y, gv.y * t.x - gv.x * t.y);
+          const float2 fv = f[e];
+          gt.x += gv.x * fv.x + gv.y * fv.y;
+          gt.y += gv.y * fv.x - gv.x * fv.y;
+        }
+        const float2 dt = cmul(t, gam);  // dt/dh
+        acc += gt.x * dt.x + gt.y * dt.y;  // Re(gt conj(dt))
+      }
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if (lane == 0) {
+      float s = red[px];
+      for (int l = 1; l < a.bl; ++l) s += red[l * PX + px];
+      G += s;
+    }
+    __syncthreads();  // red is rewritten by the next mirror position
+  }
+  if (live && lane == 0) quant_bwd_px(qa, get_dyn(qa), w, ysave, p, n, G, gw);
 }
 
 static int qargs(const thz_quant_desc* d, QArgs* a) {
@@ -472,6 +539,41 @@ extern "C" int thz_quant_forward(const thz_quant_desc* d, const float* weight, c
   KernelTimer kt("quant_fwd", s);
   const int n = d->hq * d->wq;
   hipLaunchKernelGGL(quant_fwd, dim3((n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
+  return THZ_OK;
+}
+
+extern "C" int thz_doe_quant_backward(const thz_doe_desc* d, const thz_quant_desc* q, const void* grad_out,
+                                      const void* field, const float* height, const float* noise, const float* weight,
+                                      const float* y_soft, void* grad_field, float* grad_weight, thz_stream_t stream) {
+  if (!d || !grad_out || !field || !height || !weight || !grad_weight) return fail(THZ_E_ARG, "null argument");
+  if (d->B < 1 || d->C < 1 || d->H < 1 || d->W < 1) return fail(THZ_E_ARG, "bad shape");
+  if (d->C > THZ_MAX_WAVELENGTHS) return fail(THZ_E_UNSUPPORTED, "C=%d > %d", d->C, THZ_MAX_WAVELENGTHS);
+  QArgs qa;
+  int e = qargs(q, &qa);
+  if (e) return e;
+  const int Hf = q->mirror ? 2 * q->hq : q->hq, Wf = q->mirror ? 2 * q->wq : q->wq;
+  if (d->hs != d->H || d->ws != d->W || Hf != d->H || Wf != d->W)
+    return fail(THZ_E_UNSUPPORTED, "fused DOE backward needs the quantized map at the field's size (%dx%d map, %dx%d "
+                "height, %dx%d field)", Hf, Wf, d->hs, d->ws, d->H, d->W);
+  const bool gumbel = q->kind == THZ_Q_NGS || q->kind == THZ_Q_SGV1 || (q->kind == THZ_Q_SGV3 && q->iter_frac > 0.3f);
+  if (gumbel && !y_soft) return fail(THZ_E_ARG, "null y_soft (Gumbel kinds)");
+  ModArgs a{};
+  a.B = d->B; a.C = d->C; a.H = d->H; a.W = d->W; a.hs = d->hs; a.ws = d->ws;
+  a.has_noise = noise != nullptr;
+  a.tol = d->tolerance; a.eps = d->epsilon; a.tand = d->tand;
+  a.rng = d->rng;
+  a.rng_stream = d->rng_stream;
+  for (int c = 0; c < d->C; ++c) a.lam[c] = d->wavelengths[c];
+  a.bl = 1;
+  while (a.bl < 16 && 2 * a.bl <= d->B) a.bl *= 2;  // doe_modulate_bwd's lanes: the same batch sums
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("doe_modulate_quant_bwd", s);
+  const int n = q->hq * q->wq, px = MOD_THREADS / a.bl;
+  hipLaunchKernelGGL(doe_modulate_quant_bwd, dim3((n + px - 1) / px), dim3(MOD_THREADS), 0, s,
+                     (const float2*)grad_out, (const float2*)field, height, noise, (float2*)grad_field, a, qa, weight,
+                     y_soft, grad_weight);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;

@@ -244,10 +244,13 @@ def asm_propagate(data, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, band
 class _AsmModulatedFunction(torch.autograd.Function):
     """ASM forward of DOELayer.modulate(field) in one pipeline (thz_asm_forward_modulated): the row
     pass applies t_c(h + noise) in its loader.  Backward: the ASM adjoint summed over the planes
-    (one launch), then the modulate backward kernel (grad_field, grad_height)."""
+    (one launch), then the modulate backward kernel (grad_field, grad_height) -- or, when the height
+    map comes straight from a quantizer of the field's size (doe.QuantLink), the modulate and
+    quantizer backward in one kernel (grad_field, grad_weight)."""
 
     @staticmethod
-    def forward(ctx, field, height, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev):
+    def forward(ctx, field, height, weight, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask,
+                z_dev):
         _require_device(field, "ASM")
         field = field.contiguous()
         h = height.detach().contiguous().float()
@@ -278,15 +281,36 @@ class _AsmModulatedFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
-        from . import doe as _doe
         field, h = ctx.saved_tensors
         pend = ctx.pend
         wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, mask, z_dev = ctx.cfg
         gm = asm_apply(g.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True, mask=mask,
                        z_dev=z_dev)
-        gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
-                                        ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
-        return gf, gh, None, None, None, None, None, None, None, None, None, None
+        gf, gh, gw = _doe_backward(ctx, gm, field, h, pend)
+        return (gf, gh, gw) + (None,) * 11
+
+
+def _doe_inputs(pend):
+    """(height, weight) inputs of a fused function for the pending modulation ``pend``: with a
+    fusable quantizer link (doe.QuantLink) the weight is differentiated directly, in one kernel with
+    the modulate backward (_doe_backward), and the height map enters detached."""
+    if pend.quant is None:
+        return pend.height, None
+    return pend.height.detach(), pend.quant.weight
+
+
+def _doe_backward(ctx, gm, field, h, pend):
+    """(grad_field, grad_height, grad_weight) of the modulation behind a fused function, whose
+    inputs 0, 1, 2 are (field, height, weight): one thz_doe_quant_backward when the quantizer is
+    linked, else thz_doe_modulate_backward."""
+    from . import doe as _doe
+    if pend.quant is not None and ctx.needs_input_grad[2]:
+        gf, gw = _doe.modulate_quant_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand,
+                                              pend.wavelengths, pend.quant, ctx.needs_input_grad[0], rng=pend.rng)
+        return gf, None, gw
+    gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
+                                    ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
+    return gf, gh, None
 
 
 def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=True, bandlimit="exact", mask=None,
@@ -294,7 +318,8 @@ def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=
     """Differentiable fused DOE modulation + ASM over Z planes: [B,C,H,W] -> [Z,B,C,Ho,Wo]; ``mask``
     and ``z_dev`` as asm_propagate."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
-    return _AsmModulatedFunction.apply(pend.field, pend.height, pend, list(map(float, wavelengths)),
+    height, weight = _doe_inputs(pend)
+    return _AsmModulatedFunction.apply(pend.field, height, weight, pend, list(map(float, wavelengths)),
                                        tuple(map(float, spacing)), list(map(float, zs)), int(pad_h), int(pad_w),
                                        bool(unpad), bl, mask, z_dev)
 
@@ -307,7 +332,7 @@ class _AsmLossFunction(torch.autograd.Function):
     when out is used elsewhere), then the modulate backward when a modulation was fused."""
 
     @staticmethod
-    def forward(ctx, field, height, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
+    def forward(ctx, field, height, weight, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
         ctx.set_materialize_grads(False)
         if field.dtype != torch.complex64:  # thz_asm_forward_loss reads float2 pairs
             raise TypeError(f"fused ASM loss computes in complex64 fields; got {field.dtype}")
@@ -356,11 +381,10 @@ class _AsmLossFunction(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g_out, g_loss):
-        from . import doe as _doe
         field, h, out, t4, stats = ctx.saved_tensors
         wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
         if g_loss is None and g_out is None:
-            return (None,) * 11
+            return (None,) * 12
         if g_loss is None:
             gm = asm_apply(g_out, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
         else:
@@ -382,14 +406,13 @@ class _AsmLossFunction(torch.autograd.Function):
                     ctypes.c_void_p(stats.data_ptr()), ctypes.c_void_p(g.data_ptr()),
                     ctypes.c_void_p(go.data_ptr() if go is not None else 0), ctypes.c_void_p(gm.data_ptr()),
                     ctypes.c_void_p(ws.data_ptr()), ctypes.c_size_t(ws.numel()), _stream_handle()))
-        gf = gh = None
+        gh = gw = None
         pend = ctx.pend
         if pend is None:
             gf = gm
         else:
-            gf, gh = _doe.modulate_backward(gm, field, h, pend.noise, pend.tol, pend.eps, pend.tand, pend.wavelengths,
-                                            ctx.needs_input_grad[0], ctx.needs_input_grad[1], rng=pend.rng)
-        return gf, gh, None, None, None, None, None, None, None, None, None
+            gf, gh, gw = _doe_backward(ctx, gm, field, h, pend)
+        return (gf, gh, gw) + (None,) * 9
 
 
 def asm_propagate_loss(x, target, wavelengths, spacing, z, pad_h, pad_w, unpad=True, bandlimit="exact", pend=None):
@@ -397,8 +420,8 @@ def asm_propagate_loss(x, target, wavelengths, spacing, z, pad_h, pad_w, unpad=T
     ``pend`` (doe.PendingModulation, not yet formed): propagate its modulation of ``pend.field``
     (``x`` is then ignored), as asm_propagate_modulated."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
-    field, height = (pend.field, pend.height) if pend is not None else (x, None)
-    return _AsmLossFunction.apply(field, height, target, pend, list(map(float, wavelengths)),
+    field, (height, weight) = (pend.field, _doe_inputs(pend)) if pend is not None else (x, (None, None))
+    return _AsmLossFunction.apply(field, height, weight, target, pend, list(map(float, wavelengths)),
                                   tuple(map(float, spacing)), [float(z)], int(pad_h), int(pad_w), bool(unpad), bl)
 
 

@@ -21,10 +21,11 @@ def load(d):
 
 
 def short(name):
-    n = name.split("(")[0]
-    for p in ("void ", "at::native::", "(anonymous namespace)::"):
+    n = name.replace("(anonymous namespace)::", "")
+    n = n.split("(")[0]
+    for p in ("void ", "at::native::"):
         n = n.replace(p, "")
-    return n[:70]
+    return n[:90]
 
 
 def main():

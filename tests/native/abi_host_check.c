@@ -151,6 +151,21 @@ int main(void) {
   EXPECT(thz_aperture(NULL, NULL, NULL, NULL) != THZ_OK, "aperture null");
   EXPECT(thz_doe_modulate_forward(NULL, NULL, NULL, NULL, NULL, NULL, NULL) != THZ_OK, "modulate null");
   EXPECT(thz_quant_forward(NULL, NULL, NULL, NULL, NULL, NULL) != THZ_OK, "quant null");
+  EXPECT(thz_doe_quant_backward(NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL, NULL) != THZ_OK,
+         "fused DOE backward null");
+  {  /* an upsampled height map is refused before any launch */
+    float wl = 1e-3f, lut[4] = {0.f, 0.25e-3f, 0.5e-3f, 0.75e-3f};
+    thz_doe_desc dd;
+    memset(&dd, 0, sizeof dd);
+    dd.B = 1; dd.C = 1; dd.H = 100; dd.W = 100; dd.hs = 50; dd.ws = 50; dd.epsilon = 2.66f;
+    dd.wavelengths = &wl;
+    thz_quant_desc qd;
+    memset(&qd, 0, sizeof qd);
+    qd.kind = THZ_Q_FP; qd.hq = 50; qd.wq = 50; qd.L = 4; qd.lut = lut; qd.hmax = 1e-3f;
+    EXPECT(thz_doe_quant_backward(&dd, &qd, dummy, dummy, (const float*)dummy, NULL, (const float*)dummy, NULL, NULL,
+                                  (float*)dummy, NULL) == THZ_E_UNSUPPORTED,
+           "fused DOE backward refuses an upsampled map");
+  }
   EXPECT(thz_resample_forward(NULL, NULL, NULL, NULL) != THZ_OK, "resample null");
   EXPECT(thz_radial_forward(NULL, 0, 0, 0, NULL, NULL) != THZ_OK, "radial bad");
   EXPECT(thz_fft_rows(NULL, NULL, 0, 1024, 0, NULL) != THZ_OK, "fft rows bad");

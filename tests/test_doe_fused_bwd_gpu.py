@@ -1,0 +1,160 @@
+"""The DOE layer's backward in one kernel (thz_doe_quant_backward, doe.modulate_quant_backward):
+bit-identical to the two-kernel form it replaces -- thz_doe_modulate_backward (grad_field,
+grad_height) then thz_quant_backward (grad_weight) -- for every quantizer kind, mirrored (num_unit
+set) and plain maps, batch sizes that give 1, 2, 4 and 16 batch lanes, one and two wavelengths,
+torch-drawn and device-drawn noise.  Plus the layers end to end: a quantized layer through the
+fused ASM (and the fused ASM -> loss) with the link on and forced off give the same weight
+gradient bit for bit.  (Components/QuantizedDOE.py:92-126 modulate, :286-292 / :794-860 /
+:1022-1041 / :1193-1223 / :1239-1388 / :411-456 the quantizers.)"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+C0 = 2.998e8
+MM = 1e-3
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+KINDS = ["FP", "STE", "PSQ", "SGV3_0.1", "SGV3_0.5", "SGV3_0.9", "NGS", "SGV1"]
+
+
+def _quantized(kind, mirror, dev, g, rng=None):
+    from quantizationawarethzdoe_amd import _lib, doe
+    L, hmax, lam, eps = 4, 1 * MM, C0 / 300e9, 2.66
+    lut = [hmax * i / L for i in range(L)]
+    hq = wq = 50 if mirror else 100
+    name, _, frac = kind.partition("_")
+    k = getattr(_lib, "Q_" + name)
+    shape = (hq, wq, L) if name == "NGS" else (hq, wq)
+    w = (torch.randn(shape, generator=g) * 2.0).to(dev).requires_grad_(True)
+    kw, clamp = {}, 8.0
+    gumbel = name in ("NGS", "SGV1") or (name == "SGV3" and float(frac) > 0.3)
+    if name == "SGV3":
+        clamp = 10.0
+        kw = dict(tau=2.0, c_s=100.0, s=1.25, beta=0.4, iter_frac=float(frac), phase_scale=doe.phase_scale(lam, eps))
+    elif name == "SGV1":
+        kw = dict(tau=2.0, c_s=100.0, s=1.25, phase_scale=doe.phase_scale(lam, eps))
+        clamp = 0.0
+    elif name == "NGS":
+        kw = dict(tau=1.5)
+        clamp = 0.0
+    elif name == "PSQ":
+        kw = dict(tau=40.0)
+    expo = None
+    if gumbel and rng is None:
+        eshape = (hq, wq, L) if name == "NGS" else (L, hq, wq)
+        expo = torch.empty(eshape).exponential_(generator=g).to(dev)
+    if gumbel and rng is not None:
+        eshape = (hq, wq, L) if name == "NGS" else (L, hq, wq)
+        h = doe.quantize(k, w, lut, hmax, clamp=clamp, mirror=mirror, rng=rng, expo_shape=eshape, **kw)
+    else:
+        h = doe.quantize(k, w, lut, hmax, clamp=clamp, mirror=mirror, expo=expo, **kw)
+    return w, h, eps
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("mirror", [False, True], ids=["plain", "mirror"])
+@pytest.mark.parametrize("B,C", [(1, 1), (3, 2), (32, 1)])
+def test_fused_doe_backward_bit_identical_to_two_kernels(kind, mirror, B, C):
+    from quantizationawarethzdoe_amd import doe
+    dev = _dev()
+    g = torch.Generator().manual_seed(hash((kind, mirror, B, C)) % (2 ** 31))
+    w, h, eps = _quantized(kind, mirror, dev, g)
+    link = h._thz_quant
+    wls = [C0 / 300e9, C0 / 250e9][:C]
+    field = torch.randn(B, C, 100, 100, 2, generator=g).to(dev)
+    field = torch.view_as_complex(field)
+    gout = torch.view_as_complex(torch.randn(B, C, 100, 100, 2, generator=g).to(dev))
+    noise = torch.rand(100, 100, generator=g).to(dev)
+    tol, tand = 30e-6, 0.003
+    gf1, gh = doe.modulate_backward(gout, field, h.detach(), noise, tol, eps, tand, wls)
+    (gw1,) = torch.autograd.grad(h, w, gh)
+    gf2, gw2 = doe.modulate_quant_backward(gout, field, h.detach(), noise, tol, eps, tand, wls, link)
+    assert torch.equal(gf1, gf2)
+    assert torch.equal(gw1, gw2), (gw1 - gw2).abs().max()
+    assert torch.isfinite(gw2).all()
+
+
+def test_fused_doe_backward_device_noise_bit_identical():
+    """The graph trainers' form: height noise and Gumbel draws from the device generator."""
+    from quantizationawarethzdoe_amd import doe
+    dev = _dev()
+    g = torch.Generator().manual_seed(5)
+    rng = (torch.tensor([1234, 7], dtype=torch.int32, device=dev), 3)
+    w, h, eps = _quantized("SGV3_0.5", True, dev, g, rng=(rng[0], rng[1] + 1))
+    link = h._thz_quant
+    field = torch.view_as_complex(torch.randn(8, 1, 100, 100, 2, generator=g).to(dev))
+    gout = torch.view_as_complex(torch.randn(8, 1, 100, 100, 2, generator=g).to(dev))
+    gf1, gh = doe.modulate_backward(gout, field, h.detach(), None, 30e-6, eps, 0.003, [C0 / 300e9], rng=rng)
+    (gw1,) = torch.autograd.grad(h, w, gh)
+    gf2, gw2 = doe.modulate_quant_backward(gout, field, h.detach(), None, 30e-6, eps, 0.003, [C0 / 300e9], link,
+                                           rng=rng)
+    assert torch.equal(gf1, gf2) and torch.equal(gw1, gw2)
+
+
+@pytest.mark.parametrize("loss", [False, True], ids=["asm", "asm_loss"])
+@pytest.mark.parametrize("layer", ["v3_mirror", "fp", "ngs"])
+def test_layer_through_fused_asm_link_on_and_off(monkeypatch, layer, loss):
+    """A quantized layer's weight gradient through the fused DOE -> ASM (and DOE -> ASM -> loss)
+    pipeline: with the quantizer link (one backward kernel) == without it (modulate backward, then
+    the quantizer's autograd node), bit for bit, and the field gradient too."""
+    from quantizationawarethzdoe_amd import doe, optics, propagation
+    from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    dev = _dev()
+    dp = {'doe_size': [100, 100], 'doe_dxy': 1 * MM, 'doe_level': 4, 'look_up_table': None,
+          'num_unit': 2 if layer == "v3_mirror" else None, 'height_constraint_max': 1 * MM,
+          'tolerance': 30e-6, 'material': [2.66, 0.003]}
+    op = {'c_s': 100, 'tau_max': 2.5, 'tau_min': 1.5}
+    g = torch.Generator().manual_seed(11)
+    x = torch.view_as_complex(torch.randn(2, 1, 100, 100, 2, generator=g)).to(dev)
+    target = torch.rand(1, 1, 100, 100, generator=g).to(dev)
+    expo = {}
+    unif = torch.rand(100, 100, generator=g).to(dev)
+    grads = {}
+    for linked in (True, False):
+        torch.manual_seed(0)
+        if layer == "fp":
+            lay = Q.FullPrecisionDOELayer(dp, device=dev)
+        elif layer == "ngs":
+            lay = Q.NaiveGumbelQuantizedDOELayer(dp, op, device=dev)
+        else:
+            lay = Q.SoftGumbelQuantizedDOELayerv3(dp, op, device=dev)
+
+        def fixed_expo(shape, like):
+            key = tuple(shape)
+            if key not in expo:
+                expo[key] = torch.empty(key).exponential_(generator=g).to(like.device)
+            return expo[key].clone()
+        lay._gumbel_noise = fixed_expo
+        if not linked:
+            monkeypatch.setattr(doe.QuantLink, "fusable", lambda self, f, h: False)
+        monkeypatch.setattr(torch, "rand_like", lambda t, *a, **k: unif.clone())
+        xr = x.clone().requires_grad_(True)
+        field = ElectricField(data=xr, wavelengths=C0 / 300e9, spacing=1 * MM, device=dev)
+        prop = ASM_prop(z_distance=20 * MM, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True,
+                        device=dev)
+        out = lay(field, 0.6)
+        assert (out._pending.quant is not None) == linked
+        if loss:
+            with propagation.deferred_output():
+                o = prop(out)
+            val = optics.field_intensity_mse(o, target)
+        else:
+            val = (prop(out).data.abs() ** 2).sum()
+        val.backward()
+        p = next(iter(lay.parameters()))
+        grads[linked] = (p.grad.clone(), xr.grad.clone(), float(val.detach()))
+        monkeypatch.undo()
+    assert grads[True][2] == grads[False][2]
+    assert torch.equal(grads[True][1], grads[False][1])
+    assert torch.equal(grads[True][0], grads[False][0]), (grads[True][0] - grads[False][0]).abs().max()
+    assert math.isfinite(float(grads[True][0].abs().sum()))

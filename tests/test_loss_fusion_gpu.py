@@ -166,7 +166,15 @@ def test_loss_near_convergence_vs_fp64_oracle(fused):
     ~ 1e-9 relative here; what remains is the fp32 rounding of |E|^2 itself (~6e-8 of I against
     residuals of ~1e-4), so the bound vs the fp64 oracle of the same fp32 field is 1e-2 relative
     -- a cancelling fp32 form would be off by O(1).  The loss is ~1e-8 against S_TT / n ~ 0.3.
-    Gradient (2 E dL/dI): rel-L2 <= 1e-2 on the same grounds."""
+
+    Gradient (2 E dL/dI), two references.  (a) fp64 arithmetic on the fp32 intensities the
+    reference itself forms (torch.abs(E) ** 2 of the complex64 field, on the device): rel-L2 <= 5e-3
+    (the kernels' fp32 residual r = I/m - T carries ~1e-7 of T against r ~ 1e-4 T).  (b) the fp64
+    oracle (|E|^2 in fp64): the max intensity m then differs by the fp32 rounding of I_max
+    (delta ~ 6e-8), which shifts every residual coherently by -(I/m) delta; the argmax element's
+    term S / m^2 (S = sum_i r_i I_i, a random-sign sum of n = 10^4 residuals of ~1e-4) moves by
+    ~delta sqrt(n) / 1e-4 ~ 6 %, and that element carries ~40 % of the gradient's norm here
+    (measured on the box: 1.5e-2 rel-L2, all of it at the two argmax elements).  Bound 0.1."""
     from quantizationawarethzdoe_amd import optics, propagation as P
     dev = _dev()
     g = torch.Generator().manual_seed(8)
@@ -199,10 +207,21 @@ def test_loss_near_convergence_vs_fp64_oracle(fused):
         ref = orc.intensity_mse(Eo, tgt.cpu().double())
         ref.backward()
         rg = Eo.grad
+        # (a): dL/dE = 2 E g (r / m - [argmax] S / m^2), g = 2 / N, in fp64 from the fp32 intensities
+        I32 = (E.abs() ** 2).double().cpu()
+        flat = I32.reshape(2, -1)
+        m = flat.max(dim=1).values
+        am = flat.argmax(dim=1)
+        r = flat / m[:, None] - tgt.cpu().double().reshape(2, -1)
+        S = (r * flat).sum(dim=1)
+        gI = (2.0 / flat.numel()) * r / m[:, None]
+        gI[torch.arange(2), am] -= (2.0 / flat.numel()) * S / m ** 2
+        rg32 = (2.0 * E.cpu().to(torch.complex128).reshape(2, -1) * gI).reshape(E.shape)
+        assert rel_l2(gx.cpu().numpy(), rg32.numpy()) <= 5e-3
     lv, rv = float(loss.detach()), float(ref.detach())
     assert 1e-10 < rv < 1e-6, rv  # near convergence: the loss is ~1e-8 of the target's scale
     assert abs(lv - rv) <= 1e-2 * rv, (lv, rv)
-    assert rel_l2(gx.cpu().numpy(), rg.numpy()) <= 1e-2
+    assert rel_l2(gx.cpu().numpy(), rg.numpy()) <= (1e-2 if fused else 0.1)
 
 
 @pytest.mark.parametrize("how", ["wavelength_f64", "data_c128"])
