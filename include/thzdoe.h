@@ -52,7 +52,7 @@ typedef void* thz_stream_t; /* hipStream_t */
 /* ABI of this header.  Bumped whenever a descriptor struct changes layout (round 2 appended
  * rng / rng_stream to thz_doe_desc and thz_quant_desc; 4 added thz_asm_transfer_function and
  * thz_rs_kernel, which the bindings require; 5 appended thz_asm_desc.window_mask, 6 thz_asm_desc.z_dev,
- * 7 added thz_doe_quant_backward):
+ * 7 added thz_doe_quant_backward and thz_radial_quant_backward):
  * a caller compares thz_abi_version()
  * with the THZ_ABI_VERSION it was compiled against before its first call, since a shorter
  * struct from an older header would make the library read past it.  Descriptors are plain C
@@ -283,6 +283,12 @@ int thz_doe_quant_backward(const thz_doe_desc* d, const thz_quant_desc* q, const
  */
 int thz_radial_forward(const float* profile, int R, int H, int W, float* out, thz_stream_t stream);
 int thz_radial_backward(const float* grad_out, int R, int H, int W, float* grad_profile, thz_stream_t stream);
+/* The rotationally symmetric layer's backward from the map gradient to its weight in one kernel:
+ * thz_radial_backward then thz_quant_backward of the profile quantizer q (hq * wq == R, mirror 0;
+ * weight / y_soft as thz_quant_backward), the profile gradient gathered per bin in a fixed order
+ * (deterministic; thz_radial_backward scatters with atomics). */
+int thz_radial_quant_backward(const thz_quant_desc* q, const float* grad_map, int R, int H, int W, const float* weight,
+                              const float* y_soft, float* grad_weight, thz_stream_t stream);
 
 /*
  * Optical elements around the DOE, generated / applied on the device.
@@ -347,9 +353,13 @@ int thz_intensity_mse_backward(const thz_loss_desc* d, const void* field, const 
  * 336-370, normalize = utils/Helper_Functions.py:185-193).  l describes the ASM output
  * [B, C, Ho, Wo]; out, loss and stats are what thz_asm_forward and thz_intensity_mse_forward
  * return (stats: thz_intensity_mse_workspace_size bytes, valid for thz_intensity_mse_backward).
+ * Z > 1 planes (the multi-plane notebooks, e.g. plot_data/example_2 / example_3): l describes the
+ * Z x B plane-major items [Z B, C, Ho, Wo] (each normalised by its own max; target tB in {1, Z B})
+ * and the loss is the SUM over the planes of each plane's mean -- the notebooks' summed MSEs.
  */
 /*
- * Its backward's first half in one pipeline: the ASM adjoint (d->adjoint == 1, Z == 1) of the loss
+ * Its backward's first half in one pipeline: the ASM adjoint (d->adjoint == 1; Z >= 1 with l as above,
+ * the Z-summing adjoint) of the loss
  * gradient dL/dE = 2 E dL/dI at the forward output `field` (thz_intensity_mse_backward's formula,
  * from the same target, stats and device grad_loss [1]), plus grad_out when non-NULL (the
  * cotangent of the output field itself).  The row pass forms the gradient as it loads each row.

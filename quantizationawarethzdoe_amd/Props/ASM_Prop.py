@@ -211,7 +211,8 @@ class ASM_prop(nn.Module):
         self.check_Zc = False
 
     def _run(self, field: ElectricField, zs, loss_target=None, out_mask=None, z_dev=None):
-        """[Z, B, C, Ho, Wo]; with ``loss_target`` (one z): (out, QAT loss) from the fused pipeline;
+        """[Z, B, C, Ho, Wo]; with ``loss_target``: (out, QAT loss) from the fused pipeline (Z > 1: the
+        sum of the planes' losses, propagation.asm_propagate_loss);
         ``out_mask``: an aperture folded onto the output (propagation.window_mask_fusable geometry);
         ``z_dev``: the planes read from device memory (propagation._asm_desc)."""
         pend = field._take_pending()
@@ -233,8 +234,8 @@ class ASM_prop(nn.Module):
             if loss_target is not None:
                 fuse = pend is not None and pend.out is None
                 x = pend.run() if pend is not None and not fuse else x
-                out = _prop.asm_propagate_loss(x, loss_target, wl, sp, zs[0], ph, pw, unpad=unpad, bandlimit=bl,
-                                               pend=pend if fuse else None)
+                out = _prop.asm_propagate_loss(x, loss_target, wl, sp, list(zs), ph, pw, unpad=unpad, bandlimit=bl,
+                                               pend=pend if fuse else None, z_dev=z_dev)
             elif pend is not None and pend.out is None:  # the DOE layer's modulation, fused into the row pass
                 out = _prop.asm_propagate_modulated(pend, wl, sp, zs, ph, pw, unpad=unpad, bandlimit=bl,
                                                     mask=out_mask, z_dev=z_dev)
@@ -283,6 +284,13 @@ class ASM_prop(nn.Module):
         Eout = ElectricField(data=out.squeeze(0), wavelengths=field.wavelengths, spacing=field.spacing,
                              device=field.device)
         return Eout._adopt_host(field)
+
+    def propagate_planes_loss(self, field: ElectricField, z_list, target, z_dev=None):
+        """Additive API: propagate_planes fused with the QAT loss of the multi-plane notebooks
+        (plot_data/example_2, example_3: the sum over the planes of MSE(normalize(|E_z|^2),
+        target_z)) -> (out [Z, B, C, Ho, Wo], loss []).  ``target`` [tB, tC, Ho, Wo] broadcast over
+        the Z x B plane-major items (tB in {1, Z B}).  At most THZ_MAX_Z planes."""
+        return self._run(field, _z_host(z_list), loss_target=target, z_dev=z_dev)
 
     def propagate_planes(self, field: ElectricField, z_list, z_dev=None) -> torch.Tensor:
         """Additive API: all planes of ``z_list`` in one call -> [Z, B, C, Ho, Wo].  ``z_dev``

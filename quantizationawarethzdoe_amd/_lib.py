@@ -32,7 +32,7 @@ EXPORTED = [
     "thz_czt_workspace_size", "thz_czt_forward",
     "thz_rsc_workspace_size", "thz_rsc_forward",
     "thz_doe_modulate_forward", "thz_doe_modulate_backward", "thz_quant_forward", "thz_quant_backward",
-    "thz_doe_quant_backward",
+    "thz_doe_quant_backward", "thz_radial_quant_backward",
     "thz_radial_forward", "thz_radial_backward",
     "thz_gaussian_beam", "thz_thin_lens", "thz_aperture",
     "thz_intensity_mse_workspace_size", "thz_intensity_mse_forward", "thz_intensity_mse_backward",
@@ -202,6 +202,8 @@ def _declare(lib):
     lib.thz_quant_backward.argtypes = [ctypes.POINTER(QuantDesc), c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
     lib.thz_doe_quant_backward.argtypes = [ctypes.POINTER(DoeDesc), ctypes.POINTER(QuantDesc), c_void_p, c_void_p,
                                            c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]
+    lib.thz_radial_quant_backward.argtypes = [ctypes.POINTER(QuantDesc), c_void_p, c_int, c_int, c_int, c_void_p,
+                                              c_void_p, c_void_p, c_void_p]
     lib.thz_radial_forward.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]
     lib.thz_radial_backward.argtypes = [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p]
     lib.thz_czt_workspace_size.argtypes = [ctypes.POINTER(CztDesc), ctypes.POINTER(c_size_t)]

@@ -186,7 +186,10 @@ struct Geo {
 // Compile-time mixed-radix sizes (MxPlan, one 64-thread workgroup per transform): the P = 300
 // grid of the cfg4 / cfg5 layers.  Other non-power-of-two sizes run the runtime plan.
 constexpr int MX_T = 64;
-constexpr int MX_WPE = 8;  // waves per SIMD of the mixed-radix column pass (46 VGPRs, no scratch)
+#ifndef THZ_MX_WPE
+#define THZ_MX_WPE 8
+#endif
+constexpr int MX_WPE = THZ_MX_WPE;  // waves per SIMD of the mixed-radix column pass
 __host__ __device__ constexpr bool is_mx(int n) { return n == Mx300::N; }
 
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
@@ -237,10 +240,12 @@ struct RowSrc {
     xh = ez ? lin(-(float)a.Hin * a.dx / 2.0f, (float)a.Hin * a.dx / 2.0f, a.Hin, h) : 0.f;
     hsrc = a.mod_h ? doe_nearest_src(h, a.mod_hs, a.Hin) * a.mod_ws : 0;
     lam_c = a.lam[bc % a.C];
-    // loss gradient rows: field E, target T and the statistics of batch item b
+    // loss gradient rows: field E, target T and the statistics of loss item b (the forward's plane
+    // z and batch item: b = z B + batch, the Z-summing adjoint's planes included)
     if (a.lg_field) {
-      const int b = bc / a.C, c = bc - b * a.C;
-      lg_row = a.lg_field + ((size_t)bc * a.Hin + h) * a.Win;
+      const int gp = (a.zsum ? a.zoff * a.BC : 0) + plane;
+      const int b = gp / a.C, c = gp - b * a.C;
+      lg_row = a.lg_field + ((size_t)gp * a.Hin + h) * a.Win;
       const int tb = a.lg_tB == 1 ? 0 : b, tc = a.lg_tC == 1 ? 0 : c;
       lg_t = a.lg_target + (((size_t)tb * a.lg_tC + tc) * a.Hin + h) * a.Win;
       lg_m = a.lg_stats[3 * b];
@@ -821,9 +826,10 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
   const float* trow = nullptr;
   unsigned ibase = 0;
   int lb = 0, lc = 0;
-  if constexpr (LOSS) {
-    lb = plane / a.C;
-    lc = plane - lb * a.C;
+  if constexpr (LOSS) {  // loss item lb = z B + b of the chunk's global plane
+    const int gp = a.zoff * a.BC + plane;
+    lb = gp / a.C;
+    lc = gp - lb * a.C;
     const int tb = a.ls.tB == 1 ? 0 : lb, tc = a.ls.tC == 1 ? 0 : lc;
     trow = a.ls.target + (((size_t)tb * a.ls.tC + tc) * a.Hout + r) * a.Wout;
     ibase = (unsigned)((lc * a.Hout + r) * a.Wout);
@@ -898,7 +904,10 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     fft_lds<true>(lds, pw, tid, nt);
     for (int w = tid; w < a.Wout; w += nt) put(w, lds[padx(a.out_c0 + w)]);
   }
-  if constexpr (LOSS) loss_store_part(acc, a.ls, lb, lc * a.Hout + r);  // C Hout slots per b
+  // C Hout slots per item; loss_finish_kernel reduces them (an in-kernel finish by the last
+  // workgroup of each item cost one agent-scope release fence -- an L2 writeback -- per workgroup:
+  // cfg5 chained 1.10 -> 2.12 ms at batch 256, profiles/r05_experiments.txt)
+  if constexpr (LOSS) loss_store_part(acc, a.ls, lb, lc * a.Hout + r);
 }
 
 template <int PN>
@@ -1488,7 +1497,8 @@ static int asm_forward_impl(const thz_asm_desc* d, const thz_doe_desc* m, const 
     a.lg_stats = lg_stats;
     a.lg_tB = lg->tB;
     a.lg_tC = lg->tC;
-    a.lg_two_inv_n = (float)(2.0 / ((double)lg->B * lg->C * lg->H * lg->W));
+    // the loss of a Z-plane pipeline is the sum of the planes' means (thz_asm_forward_loss)
+    a.lg_two_inv_n = (float)(2.0 * d->Z / ((double)lg->B * lg->C * lg->H * lg->W));
   }
 
   float2* T = (float2*)workspace;
@@ -1562,9 +1572,9 @@ extern "C" int thz_asm_adjoint_loss(const thz_asm_desc* d, const thz_loss_desc* 
   if (e) return e;
   if (!l || !field || !target || !stats || !grad_loss || !grad_in)
     return fail(THZ_E_ARG, "null loss descriptor / field / target / stats / grad_loss / grad_in");
-  if (!d->adjoint || d->Z != 1) return fail(THZ_E_ARG, "the fused loss adjoint takes adjoint == 1, Z == 1");
+  if (!d->adjoint) return fail(THZ_E_ARG, "the fused loss adjoint takes adjoint == 1");
   const int Ho = d->unpad ? d->H : d->H + 2 * d->pad_h, Wo = d->unpad ? d->W : d->W + 2 * d->pad_w;
-  if (l->B != d->B || l->C != d->C || l->H != Ho || l->W != Wo)
+  if (l->B != d->Z * d->B || l->C != d->C || l->H != Ho || l->W != Wo)
     return fail(THZ_E_ARG, "loss field %dx%dx%dx%d does not match the ASM output %dx%dx%dx%d", l->B, l->C, l->H, l->W,
                 d->B, d->C, Ho, Wo);
   if (!(l->tB == 1 || l->tB == l->B) || !(l->tC == 1 || l->tC == l->C))
@@ -1580,9 +1590,9 @@ extern "C" int thz_asm_forward_loss(const thz_asm_desc* d, const thz_doe_desc* m
   int e = validate(d);
   if (e) return e;
   if (!l || !target || !loss || !stats) return fail(THZ_E_ARG, "null loss descriptor / target / loss / stats");
-  if (d->adjoint || d->Z != 1) return fail(THZ_E_ARG, "the fused loss takes one forward z-plane (Z = %d)", d->Z);
+  if (d->adjoint) return fail(THZ_E_ARG, "the fused loss is forward only (thz_asm_adjoint_loss)");
   const int Ho = d->unpad ? d->H : d->H + 2 * d->pad_h, Wo = d->unpad ? d->W : d->W + 2 * d->pad_w;
-  if (l->B != d->B || l->C != d->C || l->H != Ho || l->W != Wo)
+  if (l->B != d->Z * d->B || l->C != d->C || l->H != Ho || l->W != Wo)
     return fail(THZ_E_ARG, "loss field %dx%dx%dx%d does not match the ASM output %dx%dx%dx%d", l->B, l->C, l->H, l->W,
                 d->B, d->C, Ho, Wo);
   if (!(l->tB == 1 || l->tB == l->B) || !(l->tC == 1 || l->tC == l->C))
@@ -1594,7 +1604,7 @@ extern "C" int thz_asm_forward_loss(const thz_asm_desc* d, const thz_doe_desc* m
                   m->W, d->B, d->C, d->H, d->W);
     if (m->hs < 1 || m->ws < 1) return fail(THZ_E_ARG, "bad height-map size %dx%d", m->hs, m->ws);
   }
-  const LossSink ls = loss_sink(l, target, loss, stats, l->C * l->H);
+  const LossSink ls = loss_sink(l, target, loss, stats, l->C * l->H, d->Z);
   return asm_forward_impl(d, m, m ? height : nullptr, m ? noise : nullptr, m ? height_full : nullptr, field, out,
                           workspace, workspace_bytes, stream, &ls);
 }

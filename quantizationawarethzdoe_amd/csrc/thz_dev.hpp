@@ -379,7 +379,7 @@ struct LossSink {
   float* stats;               // [B][3] + the slots above
   int B, tB, tC;
   int per_b;                  // producer slots per batch item
-  double inv_n;               // 1 / (B C H W)
+  double inv_n;               // planes / (B C H W)
   __host__ __device__ static size_t part_offset(int B) { return 16 * (size_t)B; }  // bytes
   __host__ __device__ static size_t bytes(int B, int per_b) {
     return part_offset(B) + sizeof(LossPart) * (size_t)B * per_b + 8 * (size_t)B + 8;
@@ -389,7 +389,10 @@ struct LossSink {
   __device__ unsigned long long* counter() const { return (unsigned long long*)(terms() + B); }
 };
 
-inline LossSink loss_sink(const thz_loss_desc* d, const float* target, float* loss, float* stats, int per_b) {
+// planes > 1: the loss items are Z planes x B (plane-major) and the loss is the sum of the planes'
+// means (the multi-plane notebooks' summed MSEs)
+inline LossSink loss_sink(const thz_loss_desc* d, const float* target, float* loss, float* stats, int per_b,
+                          int planes = 1) {
   LossSink ls;
   ls.target = target;
   ls.loss = loss;
@@ -398,7 +401,7 @@ inline LossSink loss_sink(const thz_loss_desc* d, const float* target, float* lo
   ls.tB = d->tB;
   ls.tC = d->tC;
   ls.per_b = per_b;
-  ls.inv_n = 1.0 / ((double)d->B * d->C * d->H * d->W);
+  ls.inv_n = (double)planes / ((double)d->B * d->C * d->H * d->W);
   return ls;
 }
 

@@ -241,13 +241,11 @@ __device__ __forceinline__ QDyn get_dyn(const QArgs& a) {
   return a.dyn ? QDyn{a.dyn[0], a.dyn[1], a.dyn[2]} : QDyn{a.tau, a.s, a.beta};
 }
 
-__global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __restrict__ expo,
-                          float* __restrict__ hfull, float* __restrict__ ysave) {
-  const QDyn q = get_dyn(a);
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = a.hq * a.wq;
-  if (p >= n) return;
-  const int i = p / a.wq, j = p - i * a.wq;
+// quantized height of quadrant pixel p (the quantizer chain of QuantizedDOE.py for a.kind); the
+// soft samples y go to ysave when it is non-null
+__device__ __forceinline__ float quant_fwd_px(const QArgs& a, const QDyn& q, const float* __restrict__ w,
+                                              const float* __restrict__ expo, int p, int n,
+                                              float* __restrict__ ysave) {
   float out;
   float y[THZ_MAX_LUT];
   if (a.kind == THZ_Q_NGS) {
@@ -255,7 +253,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
     THZ_FOR_LEVELS(l, a.L) ex[l] = expo ? expo[(size_t)p * a.L + l] : rng_exp1(a.rng, a.rng_stream, (unsigned)(p * a.L + l));
     const int arg = gumbel_soft(w + (size_t)p * a.L, ex, a.L, q.tau, y);
     out = st_value(a, y, arg);
-    THZ_FOR_LEVELS(l, a.L) ysave[(size_t)p * a.L + l] = y[l];
+    if (ysave) THZ_FOR_LEVELS(l, a.L) ysave[(size_t)p * a.L + l] = y[l];
   } else if (a.kind == THZ_Q_SGV1) {
     // the weight is the phase itself (:411-445): scores of w, Gumbel pick, LUT value
     float logits[THZ_MAX_LUT], ex[THZ_MAX_LUT];
@@ -266,7 +264,7 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
     }
     const int arg = gumbel_soft(logits, ex, a.L, q.tau, y);
     out = st_value(a, y, arg);
-    THZ_FOR_LEVELS(l, a.L) ysave[(size_t)l * n + p] = y[l];
+    if (ysave) THZ_FOR_LEVELS(l, a.L) ysave[(size_t)l * n + p] = y[l];
   } else {
     const float wc = fminf(fmaxf(w[p], -a.clampv), a.clampv);
     const float hm = a.hmax * sigm(wc);
@@ -299,9 +297,20 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
       const int arg = gumbel_soft(logits, ex, a.L, q.tau, y);
       const float qv = st_value(a, y, arg);
       out = a.iter_frac <= 0.8f ? (1.0f - q.beta) * hm + q.beta * qv : qv;
-      THZ_FOR_LEVELS(l, a.L) ysave[(size_t)l * n + p] = y[l];
+      if (ysave) THZ_FOR_LEVELS(l, a.L) ysave[(size_t)l * n + p] = y[l];
     }
   }
+  return out;
+}
+
+__global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __restrict__ expo,
+                          float* __restrict__ hfull, float* __restrict__ ysave) {
+  const QDyn q = get_dyn(a);
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int n = a.hq * a.wq;
+  if (p >= n) return;
+  const int i = p / a.wq, j = p - i * a.wq;
+  const float out = quant_fwd_px(a, q, w, expo, p, n, ysave);
   for_mirrors(a, i, j, [&](int o) { hfull[o] = out; });
 }
 
@@ -383,8 +392,10 @@ __global__ void quant_bwd(QArgs a, const float* __restrict__ w, const float* __r
 // upsampling): modulate backward (grad_field = g conj(t) for every (b, c); dL/dh per full-map
 // pixel, the batch summed over a.bl lanes in LDS exactly as doe_modulate_bwd does) and the
 // quantizer's backward of the quadrant pixel those full-map pixels mirror (for_mirrors order), so
-// grad_height never goes to memory.  Block = MOD_THREADS threads = (MOD_THREADS / a.bl) quadrant
-// pixels x a.bl batch lanes; results bit-identical to doe_modulate_bwd followed by quant_bwd.
+// grad_height never goes to memory.  Block = MOD_THREADS threads = PXQ quadrant pixels x nm mirror
+// positions x a.bl batch lanes (thread = (lane * nm + k) * PXQ + px), so a mirrored map keeps
+// one thread per (full-map pixel, lane) as the two-kernel form has; results bit-identical to
+// doe_modulate_bwd followed by quant_bwd.
 __global__ void __launch_bounds__(MOD_THREADS) doe_modulate_quant_bwd(const float2* __restrict__ g,
                                                                       const float2* __restrict__ f,
                                                                       const float* __restrict__ h,
@@ -396,46 +407,46 @@ __global__ void __launch_bounds__(MOD_THREADS) doe_modulate_quant_bwd(const floa
   __shared__ float red[MOD_THREADS];
   const int HW = a.H * a.W;
   const int n = qa.hq * qa.wq;
-  const int PX = MOD_THREADS / a.bl;
-  const int px = threadIdx.x % PX, lane = threadIdx.x / PX;
-  const int p = blockIdx.x * PX + px;
+  const int nm = qa.mirror ? 4 : 1;
+  const int PXQ = MOD_THREADS / (nm * a.bl);
+  const int px = threadIdx.x % PXQ, k = (threadIdx.x / PXQ) % nm, lane = threadIdx.x / (PXQ * nm);
+  const int p = blockIdx.x * PXQ + px;
   const bool live = p < n;
-  const int i = live ? p / qa.wq : 0, j = live ? p - i * qa.wq : 0;
-  int pos[4];
-  int nm = 0;
-  for_mirrors(qa, i, j, [&](int o) { pos[nm++] = o; });
-  float G = 0.f;
-  for (int k = 0; k < nm; ++k) {
-    float acc = 0.f;
-    if (live) {
-      const int o = pos[k];
-      const float hv = noisy_h(h, u, o, a);
-      for (int c = 0; c < a.C; ++c) {
-        float2 gam;
-        const float2 t = transmission(hv, a.lam[c], a, &gam);
-        float2 gt = make_float2(0.f, 0.f);  // sum_b g conj(f), this lane's share
-        for (int b = lane; b < a.B; b += a.bl) {
-          const size_t e = ((size_t)b * a.C + c) * HW + o;
-          const float2 gv = g[e];
-          if (gf) gf[e] = make_float2(gv.x * t.x + gv.y * t.y, gv.y * t.x - gv.x * t.y);
-          const float2 fv = f[e];
-          gt.x += gv.x * fv.x + gv.y * fv.y;
-          gt.y += gv.y * fv.x - gv.x * fv.y;
-        }
-        const float2 dt = cmul(t, gam);  // dt/dh
-        acc += gt.x * dt.x + gt.y * dt.y;  // Re(gt conj(dt))
+  float acc = 0.f;
+  if (live) {
+    const int i = p / qa.wq, j = p - i * qa.wq;
+    int o = 0, kk = 0;
+    for_mirrors(qa, i, j, [&](int oo) {
+      if (kk++ == k) o = oo;
+    });
+    const float hv = noisy_h(h, u, o, a);
+    for (int c = 0; c < a.C; ++c) {
+      float2 gam;
+      const float2 t = transmission(hv, a.lam[c], a, &gam);
+      float2 gt = make_float2(0.f, 0.f);  // sum_b g conj(f), this lane's share
+      for (int b = lane; b < a.B; b += a.bl) {
+        const size_t e = ((size_t)b * a.C + c) * HW + o;
+        const float2 gv = g[e];
+        if (gf) gf[e] = make_float2(gv.x * t.x + gv.y * t.y, gv.y * t.x - gv.x * t.y);
+        const float2 fv = f[e];
+        gt.x += gv.x * fv.x + gv.y * fv.y;
+        gt.y += gv.y * fv.x - gv.x * fv.y;
       }
+      const float2 dt = cmul(t, gam);  // dt/dh
+      acc += gt.x * dt.x + gt.y * dt.y;  // Re(gt conj(dt))
     }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    if (lane == 0) {
-      float s = red[px];
-      for (int l = 1; l < a.bl; ++l) s += red[l * PX + px];
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (live && k == 0 && lane == 0) {
+    float G = 0.f;  // quant_bwd's sum over the mirror positions of doe_modulate_bwd's lane sums
+    for (int m = 0; m < nm; ++m) {
+      float s = red[m * PXQ + px];
+      for (int l = 1; l < a.bl; ++l) s += red[(l * nm + m) * PXQ + px];
       G += s;
     }
-    __syncthreads();  // red is rewritten by the next mirror position
+    quant_bwd_px(qa, get_dyn(qa), w, ysave, p, n, G, gw);
   }
-  if (live && lane == 0) quant_bwd_px(qa, get_dyn(qa), w, ysave, p, n, G, gw);
 }
 
 static int qargs(const thz_quant_desc* d, QArgs* a) {
@@ -570,7 +581,7 @@ extern "C" int thz_doe_quant_backward(const thz_doe_desc* d, const thz_quant_des
   while (a.bl < 16 && 2 * a.bl <= d->B) a.bl *= 2;  // doe_modulate_bwd's lanes: the same batch sums
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("doe_modulate_quant_bwd", s);
-  const int n = q->hq * q->wq, px = MOD_THREADS / a.bl;
+  const int n = q->hq * q->wq, px = MOD_THREADS / ((q->mirror ? 4 : 1) * a.bl);
   hipLaunchKernelGGL(doe_modulate_quant_bwd, dim3((n + px - 1) / px), dim3(MOD_THREADS), 0, s,
                      (const float2*)grad_out, (const float2*)field, height, noise, (float2*)grad_field, a, qa, weight,
                      y_soft, grad_weight);
@@ -622,6 +633,40 @@ __global__ void radial_bwd(const float* __restrict__ g, float* __restrict__ gpro
   const int b = radial_bin(p / W, p % W, R, H, W);
   if (b >= 0) atomicAdd(gprof + b, g[p]);
 }
+
+// The rotationally symmetric layers' backward from the map gradient to the weight in one kernel:
+// one workgroup per profile bin b gathers dL/dmap over the pixels of its annulus (radial_bin ==
+// b; per map row the candidate columns come from the quadrant distance bounds, each candidate
+// re-tested with radial_bin) in a fixed order -- no atomics, no zeroed buffer -- and applies the
+// quantizer's backward to profile pixel b (quant_bwd_px).  Replaces radial_bwd's memset + atomic
+// scatter and the quant_bwd launch.
+constexpr int RQ_THREADS = 64;
+__global__ void __launch_bounds__(RQ_THREADS) radial_quant_bwd(const float* __restrict__ g, QArgs qa, int R, int H,
+                                                               int W, const float* __restrict__ w,
+                                                               const float* __restrict__ ysave,
+                                                               float* __restrict__ gw) {
+  const int b = blockIdx.x;
+  const int r0 = R - H / 2, c0 = R - W / 2;  // centre-crop offsets (radial_bin)
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < H; i += RQ_THREADS) {
+    const int fi = r0 + i;
+    const int qx = fi < R ? R - 1 - fi : fi - R;
+    if (qx > b + 1) continue;
+    // quadrant columns qy with b <= sqrt(qx^2 + qy^2) < b + 1, one column of margin each side
+    const int lo2 = b * b - qx * qx;
+    const int qlo = lo2 > 0 ? max(0, (int)sqrtf((float)lo2) - 1) : 0;
+    const int qhi = (int)sqrtf((float)((b + 1) * (b + 1) - qx * qx)) + 1;
+    for (int qy = qlo; qy <= qhi; ++qy) {
+#pragma unroll
+      for (int side = 0; side < 2; ++side) {  // fj = R - 1 - qy (left half), R + qy (right half)
+        const int j = (side == 0 ? R - 1 - qy : R + qy) - c0;
+        if (j >= 0 && j < W && radial_bin(i, j, R, H, W) == b) acc += g[(size_t)i * W + j];
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (threadIdx.x == 0) quant_bwd_px(qa, get_dyn(qa), w, ysave, b, R, acc, gw);
+}
 }  // namespace thz
 
 extern "C" int thz_radial_forward(const float* profile, int R, int H, int W, float* out, thz_stream_t stream) {
@@ -629,6 +674,27 @@ extern "C" int thz_radial_forward(const float* profile, int R, int H, int W, flo
     return fail(THZ_E_ARG, "bad radial map arguments R=%d H=%d W=%d", R, H, W);
   hipLaunchKernelGGL(radial_fwd, dim3((H * W + 255) / 256), dim3(256), 0, (hipStream_t)stream, profile, out, R, H, W);
   THZ_LAUNCH_CHECK();
+  return THZ_OK;
+}
+
+extern "C" int thz_radial_quant_backward(const thz_quant_desc* q, const float* grad_map, int R, int H, int W,
+                                         const float* weight, const float* y_soft, float* grad_weight,
+                                         thz_stream_t stream) {
+  if (!grad_map || !weight || !grad_weight || R < 1 || H < 1 || W < 1 || H > 2 * R || W > 2 * R)
+    return fail(THZ_E_ARG, "bad radial map arguments R=%d H=%d W=%d", R, H, W);
+  QArgs qa;
+  int e = qargs(q, &qa);
+  if (e) return e;
+  if (q->mirror || q->hq * q->wq != R) return fail(THZ_E_ARG, "the radial profile quantizer is %dx%d (mirror %d), "
+                                                   "not the R = %d profile", q->hq, q->wq, q->mirror, R);
+  const bool gumbel = q->kind == THZ_Q_NGS || q->kind == THZ_Q_SGV1 || (q->kind == THZ_Q_SGV3 && q->iter_frac > 0.3f);
+  if (gumbel && !y_soft) return fail(THZ_E_ARG, "null y_soft (Gumbel kinds)");
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("radial_quant_bwd", s);
+  hipLaunchKernelGGL(radial_quant_bwd, dim3(R), dim3(RQ_THREADS), 0, s, grad_map, qa, R, H, W, weight, y_soft,
+                     grad_weight);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
   return THZ_OK;
 }
 

@@ -265,10 +265,45 @@ class _Radial(torch.autograd.Function):
         return gp.reshape(shape), None, None, None
 
 
+class _RadialQuant(torch.autograd.Function):
+    """radial_map of a quantized profile, differentiated straight to the quantizer's weight: the
+    backward is one kernel (thz_radial_quant_backward) instead of the radial scatter, its memset
+    and the quantizer backward.  ``prof`` enters detached; ``weight`` is the QuantLink's."""
+
+    @staticmethod
+    def forward(ctx, weight, prof, link, R, H, W):
+        p = prof.detach().contiguous().float().reshape(-1)
+        out = torch.empty((H, W), dtype=torch.float32, device=p.device)
+        with torch.cuda.device(p.device):
+            _lib.check(_lib.lib().thz_radial_forward(_ptr(p), R, H, W, _ptr(out), _stream_handle()))
+        ctx.link, ctx.cfg = link, (R, H, W)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        link = ctx.link
+        R, H, W = ctx.cfg
+        (kind, hq, wq, mirror, lut), kw = link.desc_args()
+        d = _quant_desc(kind, hq, wq, mirror, lut, **kw)
+        gw = torch.empty_like(link.w)
+        with torch.cuda.device(g.device):
+            _lib.check(_lib.lib().thz_radial_quant_backward(ctypes.byref(d), _ptr(g.contiguous()), R, H, W,
+                                                            _ptr(link.w), _ptr(link.ysoft), _ptr(gw),
+                                                            _stream_handle()))
+        return gw.reshape(link.weight.shape), None, None, None, None, None
+
+
 def radial_map(profile, H, W):
-    """Radial profile [.., R] -> [H, W] height map (Components/QuantizedDOE.py:1409-1433)."""
+    """Radial profile [.., R] -> [H, W] height map (Components/QuantizedDOE.py:1409-1433).  A profile
+    straight from quantize() (its QuantLink, an unmirrored R-pixel map) is differentiated to the
+    quantizer's weight in one kernel (_RadialQuant)."""
     _require_device(profile, "radial map")
-    return _Radial.apply(profile, int(profile.shape[-1]), int(H), int(W))
+    R = int(profile.shape[-1])
+    link = getattr(profile, "_thz_quant", None)
+    if (link is not None and link.weight.requires_grad and not link.cfg[3]
+            and int(link.cfg[1]) * int(link.cfg[2]) == R):
+        return _RadialQuant.apply(link.weight, profile.detach(), link, R, int(H), int(W))
+    return _Radial.apply(profile, R, int(H), int(W))
 
 
 def f32(x):

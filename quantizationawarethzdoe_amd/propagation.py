@@ -325,14 +325,18 @@ def asm_propagate_modulated(pend, wavelengths, spacing, zs, pad_h, pad_w, unpad=
 
 
 class _AsmLossFunction(torch.autograd.Function):
-    """One z-plane of ASM (optionally of a pending DOE modulation) whose row-inverse pass also
-    accumulates the QAT loss mean((normalize(|E|^2) - target)^2) (thz_asm_forward_loss).
-    Outputs (out [1,B,C,Ho,Wo], loss []).  Backward: the ASM adjoint of the loss gradient of the
-    stored field, formed in the adjoint's row pass (thz_asm_adjoint_loss; plus the out cotangent
-    when out is used elsewhere), then the modulate backward when a modulation was fused."""
+    """Z z-planes of ASM (optionally of a pending DOE modulation) whose row-inverse pass also
+    accumulates the QAT loss mean((normalize(|E|^2) - target)^2) (thz_asm_forward_loss) -- for
+    Z > 1 the sum over the planes of each plane's mean, the multi-plane notebooks' summed MSEs,
+    the target [tB, tC, Ho, Wo] broadcast over the Z B plane-major items (tB in {1, Z B}).
+    Outputs (out [Z,B,C,Ho,Wo], loss []).  Backward: the ASM adjoint (summed over the planes) of the
+    loss gradient of the stored field, formed in the adjoint's row pass (thz_asm_adjoint_loss;
+    plus the out cotangent when out is used elsewhere), then the DOE layer's backward when a
+    modulation was fused."""
 
     @staticmethod
-    def forward(ctx, field, height, weight, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit):
+    def forward(ctx, field, height, weight, target, pend, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit,
+                z_dev=None):
         ctx.set_materialize_grads(False)
         if field.dtype != torch.complex64:  # thz_asm_forward_loss reads float2 pairs
             raise TypeError(f"fused ASM loss computes in complex64 fields; got {field.dtype}")
@@ -340,18 +344,19 @@ class _AsmLossFunction(torch.autograd.Function):
         field = field.contiguous()
         B, C, H, W = field.shape
         Ho, Wo = (H, W) if unpad else (H + 2 * pad_h, W + 2 * pad_w)
+        Z = len(zs)
         t4 = target.detach().float().contiguous()
         t4 = t4.reshape((1,) * (4 - t4.dim()) + tuple(t4.shape))
-        if tuple(t4.shape[-2:]) != (Ho, Wo) or t4.shape[0] not in (1, B) or t4.shape[1] not in (1, C):
-            raise ValueError(f"target {tuple(target.shape)} does not broadcast to field {(B, C, Ho, Wo)}")
-        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False)
-        ld = _lib.LossDesc(B=B, C=C, H=Ho, W=Wo, tB=t4.shape[0], tC=t4.shape[1])
+        if tuple(t4.shape[-2:]) != (Ho, Wo) or t4.shape[0] not in (1, Z * B) or t4.shape[1] not in (1, C):
+            raise ValueError(f"target {tuple(target.shape)} does not broadcast to field {(Z * B, C, Ho, Wo)}")
+        d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, False, z_dev=z_dev)
+        ld = _lib.LossDesc(B=Z * B, C=C, H=Ho, W=Wo, tB=t4.shape[0], tC=t4.shape[1])
         L = _lib.lib()
         nbytes = ctypes.c_size_t(0)
         _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
         dev = field.device
         ws = torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=dev)
-        out = torch.empty((1, B, C, Ho, Wo), dtype=torch.complex64, device=dev)
+        out = torch.empty((Z, B, C, Ho, Wo), dtype=torch.complex64, device=dev)
         loss = torch.empty((), dtype=torch.float32, device=dev)
         stats = torch.empty(L.thz_intensity_mse_workspace_size(ctypes.byref(ld)) // 4, dtype=torch.float32,
                             device=dev)
@@ -375,24 +380,25 @@ class _AsmLossFunction(torch.autograd.Function):
             pend.hfull = hfull
         ctx.save_for_backward(field, h, out, t4, stats)
         ctx.pend = pend
-        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit)
+        ctx.cfg = (wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_dev)
         ctx.ldesc = (B, C, Ho, Wo, t4.shape[0], t4.shape[1])
         return out, loss
 
     @staticmethod
     def backward(ctx, g_out, g_loss):
         field, h, out, t4, stats = ctx.saved_tensors
-        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit = ctx.cfg
+        wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, z_dev = ctx.cfg
         if g_loss is None and g_out is None:
-            return (None,) * 12
+            return (None,) * 13
         if g_loss is None:
-            gm = asm_apply(g_out, wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True)
+            gm = asm_apply(g_out.contiguous(), wavelengths, spacing, zs, pad_h, pad_w, unpad, bandlimit, True,
+                           z_dev=z_dev)
         else:
             # the loss gradient is formed in the adjoint's row pass (thz_asm_adjoint_loss)
             B, C, Ho, Wo, tB, tC = ctx.ldesc
             H, W = field.shape[-2:]
-            ld = _lib.LossDesc(B=B, C=C, H=Ho, W=Wo, tB=tB, tC=tC)
-            d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, True)
+            ld = _lib.LossDesc(B=len(zs) * B, C=C, H=Ho, W=Wo, tB=tB, tC=tC)
+            d = _asm_desc(B, C, H, W, pad_h, pad_w, unpad, bandlimit, wavelengths, spacing, zs, True, z_dev=z_dev)
             L = _lib.lib()
             nbytes = ctypes.c_size_t(0)
             _lib.check(L.thz_asm_workspace_size(ctypes.byref(d), ctypes.byref(nbytes)))
@@ -412,17 +418,23 @@ class _AsmLossFunction(torch.autograd.Function):
             gf = gm
         else:
             gf, gh, gw = _doe_backward(ctx, gm, field, h, pend)
-        return (gf, gh, gw) + (None,) * 9
+        return (gf, gh, gw) + (None,) * 10
 
 
-def asm_propagate_loss(x, target, wavelengths, spacing, z, pad_h, pad_w, unpad=True, bandlimit="exact", pend=None):
-    """Differentiable ASM to one plane fused with the QAT loss: (out [1,B,C,Ho,Wo], loss []).
-    ``pend`` (doe.PendingModulation, not yet formed): propagate its modulation of ``pend.field``
-    (``x`` is then ignored), as asm_propagate_modulated."""
+def asm_propagate_loss(x, target, wavelengths, spacing, z, pad_h, pad_w, unpad=True, bandlimit="exact", pend=None,
+                       z_dev=None):
+    """Differentiable ASM fused with the QAT loss: (out [Z,B,C,Ho,Wo], loss []).  ``z``: one
+    distance, or a list of Z planes (the loss is then the sum of the planes' means, the target
+    broadcast over the Z B plane-major items); ``z_dev`` as asm_propagate.  ``pend``
+    (doe.PendingModulation, not yet formed): propagate its modulation of ``pend.field`` (``x`` is
+    then ignored), as asm_propagate_modulated."""
     bl = _lib.BANDLIMIT[bandlimit] if not isinstance(bandlimit, int) else bandlimit
+    zs = [float(v) for v in z] if isinstance(z, (list, tuple)) else [float(z)]
+    if len(zs) > _lib.THZ_MAX_Z:
+        raise ValueError(f"the fused loss takes at most {_lib.THZ_MAX_Z} planes per call")
     field, (height, weight) = (pend.field, _doe_inputs(pend)) if pend is not None else (x, (None, None))
     return _AsmLossFunction.apply(field, height, weight, target, pend, list(map(float, wavelengths)),
-                                  tuple(map(float, spacing)), [float(z)], int(pad_h), int(pad_w), bool(unpad), bl)
+                                  tuple(map(float, spacing)), zs, int(pad_h), int(pad_w), bool(unpad), bl, z_dev)
 
 
 class _Deferral(threading.local):

@@ -208,6 +208,13 @@ class MultiPlaneSystem(nn.Module):
         field = self.doe(self.input_field, iter_frac)
         return self.props[0].propagate_planes(field, self.planes, z_dev=z_dev)
 
+    def forward_planes_loss(self, iter_frac, target, z_dev=None):
+        """forward_planes fused with the notebooks' loss, the sum over the planes of
+        MSE(normalize(|E_z|^2), target_z) (``target`` [Z B or 1, 1, H, W]): (out, loss) from one
+        pipeline whose row-inverse pass accumulates the loss (ASM_prop.propagate_planes_loss)."""
+        field = self.doe(self.input_field, iter_frac)
+        return self.props[0].propagate_planes_loss(field, self.planes, target, z_dev=z_dev)
+
     def after_forward(self):
         """Per-iteration plane update of the notebook's forward (none here; ExtendedDOFSystem)."""
 
@@ -342,6 +349,9 @@ def release_step_graph(modules):
                 for k in ("field", "height", "out", "hfull"):
                     if k in pend.__dict__:
                         setattr(pend, k, _det(getattr(pend, k)))
+                # its quantizer link holds the weight's view (doe.QuantLink.weight): the same graph
+                if getattr(pend, "quant", None) is not None:
+                    pend.quant = None
 
 
 def agreed_capture(allreduce, capture_fn):
@@ -496,11 +506,15 @@ class QATTrainer:
             # every plane from one pipeline ([Z, B, C, H, W]; backward: the Z-summing adjoint), the
             # loss kernel over the Z B planes as its batch (normalize is per plane), x Z: the sum
             # over the planes of each plane's mean
-            out = self.system.forward_planes(frac, z_dev=self._zs_graph)
+            if self.loss_fn is _optics.intensity_mse:
+                # the loss folded into the planes' row-inverse pass, summed over the planes in-kernel
+                out, loss = self.system.forward_planes_loss(frac, self.target, z_dev=self._zs_graph)
+            else:
+                out = self.system.forward_planes(frac, z_dev=self._zs_graph)
+                Z, B = out.shape[:2]
+                loss = self.loss_fn(out.reshape((Z * B,) + tuple(out.shape[2:])), self.target) * float(Z)
             if self._zs_graph is None:
                 self.system.after_forward()  # the notebook's per-iteration plane update (eager)
-            Z, B = out.shape[:2]
-            loss = _optics.intensity_mse(out.reshape((Z * B,) + tuple(out.shape[2:])), self.target) * float(Z)
         elif self.loss_fn is _optics.intensity_mse:
             # the default loss folded into the last propagation
             with _prop.deferred_output():

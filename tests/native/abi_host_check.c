@@ -168,6 +168,7 @@ int main(void) {
   }
   EXPECT(thz_resample_forward(NULL, NULL, NULL, NULL) != THZ_OK, "resample null");
   EXPECT(thz_radial_forward(NULL, 0, 0, 0, NULL, NULL) != THZ_OK, "radial bad");
+  EXPECT(thz_radial_quant_backward(NULL, NULL, 0, 0, 0, NULL, NULL, NULL, NULL) != THZ_OK, "radial quant bad");
   EXPECT(thz_fft_rows(NULL, NULL, 0, 1024, 0, NULL) != THZ_OK, "fft rows bad");
   double ms = -1.0;
   long n = -1;

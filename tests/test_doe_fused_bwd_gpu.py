@@ -158,3 +158,44 @@ def test_layer_through_fused_asm_link_on_and_off(monkeypatch, layer, loss):
     assert torch.equal(grads[True][1], grads[False][1])
     assert torch.equal(grads[True][0], grads[False][0]), (grads[True][0] - grads[False][0]).abs().max()
     assert math.isfinite(float(grads[True][0].abs().sum()))
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("R,H", [(70, 100), (12, 20), (8, 16)])
+def test_radial_quant_backward_matches_radial_then_quantizer(kind, R, H):
+    """The rotationally symmetric layers' map -> weight backward in one kernel (thz_radial_quant_
+    backward, a per-bin gather in a fixed order) == the radial scatter (atomics) then the
+    quantizer backward, within fp32 summation-order rounding (rel-L2 <= 1e-6), for every quantizer
+    kind on an R-pixel profile, the DOE crop of the layers (H = 100 of R = 70) and small maps."""
+    from quantizationawarethzdoe_amd import _lib, doe
+    dev = _dev()
+    g = torch.Generator().manual_seed(R * 31 + H)
+    L, hmax, lam, eps = 4, 1 * MM, C0 / 300e9, 2.66
+    lut = [hmax * i / L for i in range(L)]
+    name, _, frac = kind.partition("_")
+    k = getattr(_lib, "Q_" + name)
+    shape = (1, R, L) if name == "NGS" else (1, R)
+    kw, clamp = {}, 8.0
+    if name == "SGV3":
+        clamp = 10.0
+        kw = dict(tau=2.0, c_s=100.0, s=1.25, beta=0.4, iter_frac=float(frac), phase_scale=doe.phase_scale(lam, eps))
+    elif name == "SGV1":
+        kw, clamp = dict(tau=2.0, c_s=100.0, s=1.25, phase_scale=doe.phase_scale(lam, eps)), 0.0
+    elif name == "NGS":
+        kw, clamp = dict(tau=1.5), 0.0
+    elif name == "PSQ":
+        kw = dict(tau=40.0)
+    gumbel = name in ("NGS", "SGV1") or (name == "SGV3" and float(frac) > 0.3)
+    expo = None
+    if gumbel:
+        expo = torch.empty((1, R, L) if name == "NGS" else (L, 1, R)).exponential_(generator=g).to(dev)
+    w = (torch.randn(shape, generator=g) * 2.0).to(dev).requires_grad_(True)
+    gmap = torch.randn(H, H, generator=g).to(dev)
+    prof = doe.quantize(k, w, lut, hmax, clamp=clamp, expo=expo, **kw)
+    (gw1,) = torch.autograd.grad((doe.radial_map(prof, H, H) * gmap).sum(), w)   # fused
+    prof = doe.quantize(k, w, lut, hmax, clamp=clamp, expo=expo, **kw)
+    del prof._thz_quant
+    (gw2,) = torch.autograd.grad((doe.radial_map(prof, H, H) * gmap).sum(), w)   # radial, then quantizer
+    assert torch.isfinite(gw1).all()
+    den = float(gw2.norm()) or 1.0
+    assert float((gw1 - gw2).norm()) <= 1e-6 * den, float((gw1 - gw2).norm()) / den
