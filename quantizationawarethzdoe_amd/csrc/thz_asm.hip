@@ -186,10 +186,10 @@ struct Geo {
 // Compile-time mixed-radix sizes (MxPlan, one 64-thread workgroup per transform): the P = 300
 // grid of the cfg4 / cfg5 layers.  Other non-power-of-two sizes run the runtime plan.
 constexpr int MX_T = 64;
-#ifndef THZ_MX_WPE
-#define THZ_MX_WPE 8
-#endif
-constexpr int MX_WPE = THZ_MX_WPE;  // waves per SIMD of the mixed-radix column pass
+// waves per SIMD of the mixed-radix column pass: 6 lets it keep its 70 VGPRs (8 spilled 5 of them
+// to scratch): cfg5 chained batch 256 0.986 -> 0.952 ms, dual-plane 0.080 -> 0.077 ms per step,
+// batch 32 0.290 -> 0.296 (profiles/r05_experiments.txt 4)
+constexpr int MX_WPE = 6;
 __host__ __device__ constexpr bool is_mx(int n) { return n == Mx300::N; }
 
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {

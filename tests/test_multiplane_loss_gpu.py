@@ -44,7 +44,8 @@ def test_plain_field_multiplane_loss_fused_equals_separate(H, ps, Z, B, shared):
     lref = optics.intensity_mse(ref.reshape((Z * B, 1, H, H)), tgt) * float(Z)
     lref.backward()
     assert torch.equal(out.detach(), ref.detach())
-    assert abs(float(loss) - float(lref)) <= 1e-6 * abs(float(lref)), (float(loss), float(lref))
+    lv, rv = float(loss.detach()), float(lref.detach())
+    assert abs(lv - rv) <= 1e-6 * abs(rv), (lv, rv)
     assert rel_l2(xf.grad.cpu().numpy(), xs.grad.cpu().numpy()) <= 1e-5
 
 
