@@ -87,12 +87,27 @@ def modulate_quant_backward(g, field, height, noise, tol, eps, tand, wavelengths
     q = _quant_desc(kind, hq, wq, mirror, lut, **kw)
     g = g.contiguous()
     gf = torch.empty_like(field) if need_field else None
-    gw = torch.empty_like(link.w)
+    gw = grad_slot(link.param, link.w)
     with torch.cuda.device(field.device):
         _lib.check(_lib.lib().thz_doe_quant_backward(ctypes.byref(d), ctypes.byref(q), _ptr(g), _ptr(field),
                                                      _ptr(height), _ptr(noise), _ptr(link.w), _ptr(link.ysoft),
                                                      _ptr(gf), _ptr(gw), _stream_handle()))
     return gf, gw.reshape(link.weight.shape)
+
+
+def grad_slot(weight, like):
+    """A fresh tensor for the gradient of ``weight`` (shape / dtype of ``like``): a view of its slice
+    of the trainer's all-reduce bucket when one was registered (qat.GradientAllReduce sets
+    ``weight._thz_grad_slot``) -- autograd then adopts it as ``weight.grad`` without a copy and the
+    bucket needs no packing -- else a new buffer.  The slice is handed out only while ``weight``
+    has no gradient yet and only once per backward (a second contribution, or one onto an existing
+    gradient, is accumulated into it by autograd and must not alias it)."""
+    slot = getattr(weight, "_thz_grad_slot", None) if weight is not None else None
+    if slot is not None and like.dtype == torch.float32 and weight.grad is None and id(weight) not in slot[2]:
+        flat, off, used = slot
+        used.add(id(weight))
+        return flat[off:off + like.numel()].view(like.shape)
+    return torch.empty_like(like)
 
 
 class QuantLink:
@@ -101,8 +116,9 @@ class QuantLink:
     the weight tensor it differentiates (``weight``), its fp32 contiguous copy (``w``), the saved
     soft samples (``ysoft``) and the quantizer's configuration."""
 
-    def __init__(self, cfg, weight, w, ysoft, full_shape):
+    def __init__(self, cfg, weight, w, ysoft, full_shape, param=None):
         self.cfg, self.weight, self.w, self.ysoft, self.full_shape = cfg, weight, w, ysoft, tuple(full_shape)
+        self.param = param  # the leaf tensor the weight views (its all-reduce slot: grad_slot)
 
     def desc_args(self):
         kind, hq, wq, mirror, lut, kw = self.cfg
@@ -242,7 +258,7 @@ def quantize(kind, weight, lut, hmax, clamp=8.0, mirror=False, expo=None, dyn=No
     wv = weight.reshape(shape)
     keep = {}
     h = _Quantize.apply(wv, e, cfg, tuple(expo_shape) if expo is None and expo_shape else None, keep)
-    h._thz_quant = QuantLink(cfg, wv, keep["w"], keep["ysoft"], h.shape)
+    h._thz_quant = QuantLink(cfg, wv, keep["w"], keep["ysoft"], h.shape, param=weight)
     return h
 
 
@@ -285,7 +301,7 @@ class _RadialQuant(torch.autograd.Function):
         R, H, W = ctx.cfg
         (kind, hq, wq, mirror, lut), kw = link.desc_args()
         d = _quant_desc(kind, hq, wq, mirror, lut, **kw)
-        gw = torch.empty_like(link.w)
+        gw = grad_slot(link.param, link.w)
         with torch.cuda.device(g.device):
             _lib.check(_lib.lib().thz_radial_quant_backward(ctypes.byref(d), _ptr(g.contiguous()), R, H, W,
                                                             _ptr(link.w), _ptr(link.ysoft), _ptr(gw),

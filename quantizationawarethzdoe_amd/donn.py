@@ -224,15 +224,17 @@ class DONNTrainer:
     def step(self, u, labels, iter_frac=None):
         """One iteration on images ``u`` [B, 1, H, W] (float, this rank's share) and int64 ``labels`` [B]."""
         frac = self.itr / self.max_itrs if iter_frac is None else iter_frac
-        u = u.to(self.model.device, torch.float32)
-        target = self.targets.index_select(0, labels.to(self.model.device))
+        labels = labels.to(self.model.device)
         if self.graph:
-            loss = self._graph_step(u, target, frac)
-        else:
-            self.optimizer.zero_grad(set_to_none=False)
-            loss = self._fb(u, target, frac)
-            self.allreduce.reduce()
-            self._opt()
+            loss = self._graph_step(u, labels, frac)
+            self.itr += 1
+            return loss
+        u = u.to(self.model.device, torch.float32)
+        target = self.targets.index_select(0, labels)
+        self.optimizer.zero_grad(set_to_none=False)
+        loss = self._fb(u, target, frac)
+        self.allreduce.reduce()
+        self._opt()
         self.itr += 1
         return loss
 
@@ -287,13 +289,18 @@ class DONNTrainer:
                 self._opt()
         return g_fb, g_opt, loss
 
-    def _graph_step(self, u, target, frac):
+    def _graph_step(self, u, labels, frac):
+        # the static inputs: the batch already as the complex64 field the encoder propagates (the copy
+        # converts, so the captured step has no conversion kernel) and the targets gathered straight
+        # into their buffer (one kernel, no gather + copy)
+        shape = (u.shape[0],) + tuple(self.targets.shape[1:])
         if self._static is None or self._static[0].shape != u.shape:
-            self._static = (torch.empty_like(u), torch.empty_like(target))
+            self._static = (torch.empty(u.shape, dtype=torch.complex64, device=self.model.device),
+                            torch.empty(shape, dtype=self.targets.dtype, device=self.model.device))
             self._graphs = {}
         su, st = self._static
         su.copy_(u)
-        st.copy_(target)
+        torch.index_select(self.targets, 0, labels, out=st)
         lead = self.model.does[0]
         phase = lead._graph_phase(frac)
         self._step_state.upload(lead._dyn_values(frac), self.itr)

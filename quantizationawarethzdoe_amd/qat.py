@@ -400,40 +400,58 @@ class GradientAllReduce:
         n = sum(p.numel() for p in self.params)
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.flat = torch.zeros(n, dtype=torch.float32, device=dev)
-
-    def pack(self):
-        """Gradients -> the flat bucket (a parameter without a gradient contributes zeros)."""
-        if not self.active:
-            return
+        self._offsets = []
+        self._slots_used = set()  # parameters whose slot a backward kernel took this step (doe.grad_slot)
         off = 0
         for p in self.params:
+            self._offsets.append(off)
+            if self.active and p.dtype == torch.float32:
+                # the DOE layers' fused backward kernels write this parameter's gradient straight into
+                # its slice of the bucket (doe.grad_slot): pack and unpack then copy nothing
+                p._thz_grad_slot = (self.flat, off, self._slots_used)
+            off += p.numel()
+
+    def _in_bucket(self, p, off):
+        g = p.grad
+        return (g is not None and g.dtype == torch.float32 and g.is_contiguous()
+                and g.data_ptr() == self.flat.data_ptr() + 4 * off)
+
+    def pack(self):
+        """Gradients -> the flat bucket (a parameter without a gradient contributes zeros; one whose
+        gradient a fused kernel already wrote into its slice costs nothing)."""
+        if not self.active:
+            return
+        self._slots_used.clear()  # the step's backward is done: the slots are free for the next one
+        for p, off in zip(self.params, self._offsets):
             k = p.numel()
             if p.grad is None:
                 self.flat[off:off + k].zero_()
-            else:
+            elif not self._in_bucket(p, off):
                 self.flat[off:off + k].copy_(p.grad.reshape(-1))
-            off += k
 
     def reduce(self):
-        """The one collective of the step: sum over ranks, then / world."""
+        """The one collective of the step: the mean over ranks (RCCL's average in one kernel; gloo:
+        sum, then / world)."""
         if not self.active:
             return
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.mul_(1.0 / self.world)
+        if dist.get_backend(self.group) == "nccl":
+            dist.all_reduce(self.flat, op=dist.ReduceOp.AVG, group=self.group)
+        else:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+            self.flat.mul_(1.0 / self.world)
 
     def unpack(self):
-        """The averaged bucket -> every parameter's gradient."""
+        """The averaged bucket -> every parameter's gradient (nothing to copy for a gradient that
+        is the bucket's own slice)."""
         if not self.active:
             return
-        off = 0
-        for p in self.params:
+        for p, off in zip(self.params, self._offsets):
             k = p.numel()
             g = self.flat[off:off + k].view_as(p)
             if p.grad is None:
                 p.grad = g.clone()
-            else:
+            elif not self._in_bucket(p, off):
                 p.grad.copy_(g)
-            off += k
 
     def __call__(self):
         self.pack()

@@ -129,3 +129,30 @@ def test_captured_trainers_keep_no_autograd_graph_alive(which):
     assert loss.grad_fn is None and torch.isfinite(loss)
     for d in layers:
         assert getattr(d, "height_map").grad_fn is None
+
+
+@pytest.mark.parametrize("graph", [False, True], ids=["eager", "graph"])
+def test_fused_backward_writes_gradients_into_the_allreduce_bucket(one_rank_rccl, graph):
+    """With an active all-reduce the DOE layers' fused backward kernels write each weight's gradient
+    into its slice of the flat bucket (doe.grad_slot), so pack / unpack copy nothing: after a step
+    every DONN weight's .grad IS its bucket slice, and the trajectory equals the run without the
+    collective (RCCL average over one rank), eager (zero_grad keeps the gradient tensors) and graph."""
+    from quantizationawarethzdoe_amd import donn
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(4)
+    u = torch.rand(8, 1, 100, 100, generator=g).to(dev)
+    labels = torch.randint(0, 10, (8,), generator=g).to(dev)
+    targets = donn.detector_targets(device=dev)
+    res = {}
+    for force in (False, True):
+        torch.manual_seed(2)
+        model = donn.DONN(device=dev)
+        tr = donn.DONNTrainer(model, targets, graph=graph, force_collective=force, device_rng=False)
+        losses = [float(tr.step(u, labels, 0.5)) for _ in range(4)]
+        res[force] = (losses, [p.detach().clone() for p in tr.params])
+        if force:
+            flat = tr.allreduce.flat
+            for p, off in zip(tr.allreduce.params, tr.allreduce._offsets):
+                assert p.grad is not None and p.grad.data_ptr() == flat.data_ptr() + 4 * off
+    assert res[True][0] == res[False][0]
+    assert all(torch.equal(a, b) for a, b in zip(res[True][1], res[False][1]))
