@@ -164,9 +164,10 @@ def test_layer_through_fused_asm_link_on_and_off(monkeypatch, layer, loss):
 @pytest.mark.parametrize("R,H", [(70, 100), (12, 20), (8, 16)])
 def test_radial_quant_backward_matches_radial_then_quantizer(kind, R, H):
     """The rotationally symmetric layers' map -> weight backward in one kernel (thz_radial_quant_
-    backward, a per-bin gather in a fixed order) == the radial scatter (atomics) then the
-    quantizer backward, within fp32 summation-order rounding (rel-L2 <= 1e-6), for every quantizer
-    kind on an R-pixel profile, the DOE crop of the layers (H = 100 of R = 70) and small maps."""
+    backward, a per-bin gather in a fixed order) == the radial scatter (atomics, in whatever order
+    they land) then the quantizer backward, within fp32 summation-order rounding (rel-L2 <= 1e-5:
+    a bin sums up to ~8 R signed terms; measured up to 1.05e-6), for every quantizer kind on an
+    R-pixel profile, the DOE crop of the layers (H = 100 of R = 70) and small maps."""
     from quantizationawarethzdoe_amd import _lib, doe
     dev = _dev()
     g = torch.Generator().manual_seed(R * 31 + H)
@@ -198,4 +199,4 @@ def test_radial_quant_backward_matches_radial_then_quantizer(kind, R, H):
     (gw2,) = torch.autograd.grad((doe.radial_map(prof, H, H) * gmap).sum(), w)   # radial, then quantizer
     assert torch.isfinite(gw1).all()
     den = float(gw2.norm()) or 1.0
-    assert float((gw1 - gw2).norm()) <= 1e-6 * den, float((gw1 - gw2).norm()) / den
+    assert float((gw1 - gw2).norm()) <= 1e-5 * den, float((gw1 - gw2).norm()) / den
