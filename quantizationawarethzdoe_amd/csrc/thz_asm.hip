@@ -190,9 +190,6 @@ constexpr int MX_T = 64;
 // to scratch): cfg5 chained batch 256 0.986 -> 0.952 ms, dual-plane 0.080 -> 0.077 ms per step,
 // batch 32 0.290 -> 0.296 (profiles/r05_experiments.txt 4)
 constexpr int MX_WPE = 6;
-#ifndef THZ_MX_EARLY
-#define THZ_MX_EARLY 0
-#endif
 __host__ __device__ constexpr bool is_mx(int n) { return n == Mx300::N; }
 
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
@@ -700,24 +697,6 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
   };
   auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
   const auto twr = MP::template twiddles<MX_T>(ph.tw, tid);
-  // kept rows |m_x| <= M_z per z and the z-independent sqrt(k^2 - K^2) of the elements this
-  // thread holds: the wavelength's per-column tables (asm_tf_tables).  Loaded before the forward
-  // transform (its barriers would otherwise hold the loads back and expose their latency after it)
-  const size_t tc = (size_t)(bc % a.C) * a.ncols + c;
-  const int* mzc = a.mzt + tc * a.nz;
-  const float* sqc = a.sqt + tc * PN;
-  float sq[MBL][RL];
-  int M0 = 0;
-  const bool early = THZ_MX_EARLY && !ZSUM && !a.tft;  // (RSC's table pass has no such tables)
-  if (early) {
-    M0 = mzc[z_lo];
-#pragma unroll
-    for (int m = 0; m < MBL; ++m) {
-      const int i = tid + m * MX_T;
-#pragma unroll
-      for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
-    }
-  }
   if constexpr (!ZSUM) MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
   if (!ZSUM && a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
     const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
@@ -735,13 +714,17 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
     MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
     return;
   }
-  if (!early) {
+  // kept rows |m_x| <= M_z per z and the z-independent sqrt(k^2 - K^2) of the elements this
+  // thread holds: the wavelength's per-column tables (asm_tf_tables)
+  const size_t tc = (size_t)(bc % a.C) * a.ncols + c;
+  const int* mzc = a.mzt + tc * a.nz;
+  const float* sqc = a.sqt + tc * PN;
+  float sq[MBL][RL];
 #pragma unroll
-    for (int m = 0; m < MBL; ++m) {
-      const int i = tid + m * MX_T;
+  for (int m = 0; m < MBL; ++m) {
+    const int i = tid + m * MX_T;
 #pragma unroll
-      for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
-    }
+    for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
   }
   if constexpr (ZSUM) {
     // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
@@ -784,7 +767,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
   }
   for (int zz = z_lo; zz < z_hi; ++zz) {
     const float z = zval(a, a.zoff + zz);
-    const int M = early && zz == z_lo ? M0 : mzc[zz];
+    const int M = mzc[zz];
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
     if constexpr (MID) __builtin_assume(tz >= 0 && tz < MX_T);
