@@ -184,7 +184,7 @@ def check_czt(out, idx):
             "planes_checked": len(planes), "reference": "tests/golden/cfg3_check.npz (fp64)"}
 
 
-def bench_czt(dev, rank, world, steps=10, warmup=2, dist=None):
+def bench_czt(dev, rank, world, steps=30, warmup=3, dist=None):
     """cfg3 (secondary line): CZT 2048^2 -> 512^2 zoom (dx 0.5 -> 0.25 mm, z 0.5 m) at 32
     wavelengths c0 / linspace(220, 330 GHz) of seeded white input planes (cfg3_input); the
     wavelengths are sharded over the ranks (strong scaling, no collective).  Every output plane of
@@ -486,7 +486,7 @@ def check_donn(dev, chained):
             "batch": int(u.shape[0]), "reference": "tests/golden/cfg5_check.npz (fp64)"}
 
 
-def bench_donn(dev, rank, world, steps=20, warmup=3, dist=None):
+def bench_donn(dev, rank, world, steps=100, warmup=5, dist=None):
     """cfg5 (secondary line): 3-layer DONN (100^2 fields, ASM P = 300 between layers, the
     FullPrecision DOE layers the notebook instantiates) training step on a global batch of 256
     split over the ranks: forward, detector-target loss, backward, one-bucket gradient all-reduce
