@@ -57,6 +57,59 @@ def test_gradient_allreduce_gloo_world2():
     assert all(ok and has for _, ok, has in res), res
 
 
+def _slot_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from quantizationawarethzdoe_amd import doe
+        from quantizationawarethzdoe_amd.qat import GradientAllReduce
+        params = [torch.nn.Parameter(torch.zeros(5, 6)), torch.nn.Parameter(torch.zeros(7))]
+        ar = GradientAllReduce(params)
+        g = torch.Generator().manual_seed(10 + rank)
+        vals = [torch.randn(p.shape, generator=g) for p in params]
+        # what a fused backward kernel does: take the parameter's slot, write the gradient into it;
+        # autograd then adopts the tensor as .grad (here: assigned)
+        slot = doe.grad_slot(params[0], params[0])
+        slot.copy_(vals[0])
+        params[0].grad = slot
+        in_bucket = ar._in_bucket(params[0], ar._offsets[0])
+        # a second contribution in the same backward does not get the slot again
+        second = doe.grad_slot(params[0], params[0])
+        fresh = second.data_ptr() != slot.data_ptr()
+        params[1].grad = vals[1].clone()  # an ordinary gradient is packed by a copy
+        ar()
+        out = [torch.zeros_like(v) for v in vals]
+        ok = True
+        for v, o, p in zip(vals, out, params):
+            got = [torch.zeros_like(v) for _ in range(world)]
+            dist.all_gather(got, v)
+            ok &= torch.allclose(p.grad, torch.stack(got).mean(0), atol=1e-7)
+        # after pack the slots are free again
+        again = doe.grad_slot(params[0], torch.empty(0)) if params[0].grad is None else None
+        q.put((rank, bool(in_bucket), bool(fresh), bool(ok), params[0].grad.data_ptr() == slot.data_ptr(),
+               again is None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gradient_slots_in_the_allreduce_bucket_gloo_world2():
+    """The fused DOE backward kernels write a weight's gradient straight into its slice of the
+    all-reduce bucket (doe.grad_slot): pack then copies nothing for it, the average lands in the
+    same tensor, a second request in one backward gets a fresh buffer, and ordinary gradients are
+    still packed and unpacked by copies."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_slot_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(all(r[1:]) for r in res), res
+
+
 def _agree_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
