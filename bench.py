@@ -626,6 +626,10 @@ class Ranks:
         if self.world > 1:
             import torch.distributed as dist
             if backend == "nccl":
+                # no event reuse in the PG's watchdog: a captured collective's end event handed back to
+                # an eager work made the watchdog's query fail once ("operation not permitted on an
+                # event last recorded in a capturing stream", test_collective_capture_gpu, round 5)
+                os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
                 dist.init_process_group("nccl", device_id=self.dev)
             else:
                 dist.init_process_group(backend)

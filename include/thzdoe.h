@@ -52,13 +52,14 @@ typedef void* thz_stream_t; /* hipStream_t */
 /* ABI of this header.  Bumped whenever a descriptor struct changes layout (round 2 appended
  * rng / rng_stream to thz_doe_desc and thz_quant_desc; 4 added thz_asm_transfer_function and
  * thz_rs_kernel, which the bindings require; 5 appended thz_asm_desc.window_mask, 6 thz_asm_desc.z_dev,
- * 7 added thz_doe_quant_backward and thz_radial_quant_backward):
+ * 7 added thz_doe_quant_backward and thz_radial_quant_backward, 8 thz_step_fetch and
+ * thz_adam_step):
  * a caller compares thz_abi_version()
  * with the THZ_ABI_VERSION it was compiled against before its first call, since a shorter
  * struct from an older header would make the library read past it.  Descriptors are plain C
  * structs: zero-initialise them (memset / `= {0}` / ctypes defaults) so fields a caller does not
  * know about stay 0 (no noise buffer and no device generator means no noise). */
-#define THZ_ABI_VERSION 7
+#define THZ_ABI_VERSION 8
 
 /* Library identity. */
 const char* thz_version(void);
@@ -442,6 +443,48 @@ int thz_rsc64_forward(const thz_rsc_desc64* d, const void* in, void* out, void* 
 
 /* Batched 1-D FFT of complex128 rows (as thz_fft_rows), n <= 8192. */
 int thz_fft64_rows(const void* in, void* out, int rows, int n, int inverse, thz_stream_t stream);
+
+/*
+ * Per-step state of the graph-replayed trainers (not part of the reference: qat.py StepState, the
+ * schedule values tau / s / beta, the device generator's seed and step, the multi-plane systems'
+ * plane distances, as int32 bit patterns).  ring: [depth][width] int32 in pinned host memory
+ * (hipHostMalloc'd, device-mapped), one slot filled by the host per replay; counter: device int32 [1],
+ * the fetches so far.  Copies slot (counter mod depth) into state (device [width] int32) and
+ * increments counter -- a step's graph captures it as its first node, so every replay reads the
+ * slot its host call filled without a host->device copy command between replays.  The caller
+ * rewrites a slot only after the replay that read it has run.  1 <= width <= 64.
+ */
+int thz_step_fetch(const int* ring, int depth, int width, int* state, int* counter, thz_stream_t stream);
+
+/*
+ * One Adam / AdamW step over up to THZ_MAX_ADAM_PARAMS fp32 parameters in one launch (the trainers'
+ * optimiser, quantizationawarethzdoe_amd/optim.py; the reference's notebooks step torch.optim.Adam /
+ * AdamW, e.g. plot_data/example_1/experiment_four_focal_spots.ipynb cells 22, 33, 52).  Per element,
+ * torch's single-tensor update with t = *step + 1 (each parameter's own device step count,
+ * incremented by the launch); the scalars (1 - b1, 1 - b2, 1 - lr wd, the bias corrections) formed
+ * in fp64 and rounded to fp32, as torch forms them in Python:
+ *   decoupled (AdamW): p *= 1 - lr wd;   else g += wd p
+ *   m = lerp(m, g, 1 - b1);   v = v b2 + (1 - b2) g g
+ *   p += -(lr / (1 - b1^t)) m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+ * done: device u32 [1], zero before the first launch (the launch leaves it zero): the last
+ * workgroup to finish advances the step counts, after every workgroup has read them.
+ */
+#define THZ_MAX_ADAM_PARAMS 16
+typedef struct thz_adam_param {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* step;      /* device [1] */
+  long long n;      /* elements */
+} thz_adam_param;
+typedef struct thz_adam_desc {
+  double lr, beta1, beta2, eps, weight_decay;
+  int decoupled;    /* 1: AdamW */
+  int nparams;      /* 1 .. THZ_MAX_ADAM_PARAMS */
+  unsigned* done;   /* device [1] */
+} thz_adam_desc;
+int thz_adam_step(const thz_adam_desc* d, const thz_adam_param* params, thz_stream_t stream);
 
 /*
  * Per-kernel HIP-event timing used by bench.py (not part of the reference): when

@@ -20,7 +20,7 @@ THZ_E_WORKSPACE = 3
 THZ_E_HIP = 4
 THZ_MAX_WAVELENGTHS = 64
 THZ_MAX_Z = 256
-THZ_ABI_VERSION = 7  # include/thzdoe.h: the descriptor layouts below
+THZ_ABI_VERSION = 8  # include/thzdoe.h: the descriptor layouts below
 
 BANDLIMIT = {None: 0, False: 0, "none": 0, "exact": 1, "approx": 2}
 
@@ -40,6 +40,7 @@ EXPORTED = [
     "thz_fft_rows",
     "thz_asm64_workspace_size", "thz_asm64_forward", "thz_czt64_workspace_size", "thz_czt64_forward",
     "thz_rsc64_workspace_size", "thz_rsc64_forward", "thz_fft64_rows",
+    "thz_step_fetch", "thz_adam_step",
     "thz_timing_enable", "thz_timing_reset", "thz_timing_read",
 ]
 
@@ -168,6 +169,21 @@ class ResampleDesc(ctypes.Structure):
                 ("dx_out", ctypes.c_float), ("dy_out", ctypes.c_float)]
 
 
+THZ_MAX_ADAM_PARAMS = 16
+
+
+class AdamParam(ctypes.Structure):
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("step", ctypes.c_void_p), ("n", ctypes.c_longlong)]
+
+
+class AdamDesc(ctypes.Structure):
+    _fields_ = [("lr", ctypes.c_double), ("beta1", ctypes.c_double), ("beta2", ctypes.c_double),
+                ("eps", ctypes.c_double), ("weight_decay", ctypes.c_double), ("decoupled", ctypes.c_int),
+                ("nparams", ctypes.c_int),
+                ("done", ctypes.c_void_p)]
+
+
 APERTURE_RECT, APERTURE_CIRC = 1, 2
 
 Q_FP, Q_STE, Q_PSQ, Q_SGV3, Q_NGS, Q_SGV1 = 0, 1, 2, 3, 4, 5
@@ -225,6 +241,8 @@ def _declare(lib):
         getattr(lib, f"thz_{tag}_forward").argtypes = [ctypes.POINTER(desc), c_void_p, c_void_p, c_void_p, c_size_t,
                                                        c_void_p]
     lib.thz_fft64_rows.argtypes = [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]
+    lib.thz_step_fetch.argtypes = [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]
+    lib.thz_adam_step.argtypes = [ctypes.POINTER(AdamDesc), ctypes.POINTER(AdamParam), c_void_p]
     lib.thz_timing_enable.argtypes = [c_int]
     lib.thz_timing_reset.argtypes = []
     lib.thz_timing_read.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_long)]

@@ -301,6 +301,103 @@ static bool loss_args(const thz_loss_desc* d, LossArgs* a) {
   return true;
 }
 
+// one slot of the host ring -> the device step state; the ring is read with system-scope loads
+// (pinned host memory, never cached), the counter advanced by lane 0.  Rings of <= 64 slots of
+// <= 16 values: lane l reads slot l's row beside the counter load (one round trip to host memory
+// instead of two in sequence), the counter's slot is broadcast from its lane.
+constexpr int ADAM_THREADS = 256, ADAM_PER = 1, ADAM_CHUNK = ADAM_THREADS * ADAM_PER;
+struct AdamArgs {
+  float* p[THZ_MAX_ADAM_PARAMS];
+  const float* g[THZ_MAX_ADAM_PARAMS];
+  float* m[THZ_MAX_ADAM_PARAMS];
+  float* v[THZ_MAX_ADAM_PARAMS];
+  float* step[THZ_MAX_ADAM_PARAMS];
+  long long n[THZ_MAX_ADAM_PARAMS];
+  int blk0[THZ_MAX_ADAM_PARAMS + 1];  // first workgroup of each parameter
+  int np;
+  double lr, b1, b2;
+  float omb1, b2f, omb2, eps, wd, decay;  // fp32 roundings of 1 - b1, b2, 1 - b2, eps, wd, 1 - lr wd
+  int decoupled;
+  unsigned* done;
+};
+
+// the element update (torch's single-tensor Adam expressions, fp32)
+__device__ __forceinline__ void adam_elem(const AdamArgs& a, int q, long long i, float nstep, float bc2s) {
+  float p = a.p[q][i], g = a.g[q][i];
+  if (a.decoupled) p = p * a.decay;
+  else if (a.wd != 0.0f) g = g + a.wd * p;
+  const float m0 = a.m[q][i];  // lerp(m0, g, w) as ATen evaluates it
+  const float w = a.omb1;
+  const float m = w < 0.5f ? m0 + w * (g - m0) : g - (g - m0) * (1.0f - w);
+  const float v = a.v[q][i] * a.b2f + (a.omb2 * g) * g;
+  a.m[q][i] = m;
+  a.v[q][i] = v;
+  a.p[q][i] = p + nstep * (m / (sqrtf(v) / bc2s + a.eps));
+}
+
+// A workgroup is ADAM_CHUNK elements of one parameter (one per thread: a one-workgroup loop over a
+// 2,500-element map ran 2-3x longer, its loads in sequence).  Thread q < np reads parameter q's step
+// count and forms its scalars (fp64 bias corrections); the last workgroup to finish advances the
+// counts, after every workgroup has read them.
+__global__ void __launch_bounds__(ADAM_THREADS) adam_step_kernel(AdamArgs a) {
+  __shared__ float s_ns[THZ_MAX_ADAM_PARAMS], s_bs[THZ_MAX_ADAM_PARAMS];
+  __shared__ int s_last;
+  const int tid = threadIdx.x;
+  float t = 0.0f;
+  if (tid < a.np) {
+    t = a.step[tid][0] + 1.0f;
+    const double bc1 = 1.0 - pow(a.b1, (double)t), bc2 = 1.0 - pow(a.b2, (double)t);
+    s_ns[tid] = (float)(-(a.lr / bc1));
+    s_bs[tid] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const int bid = blockIdx.x;
+  int q = 0;
+  while (q + 1 < a.np && bid >= a.blk0[q + 1]) ++q;
+  const long long i0 = (long long)(bid - a.blk0[q]) * ADAM_CHUNK + tid;
+#pragma unroll
+  for (int k = 0; k < ADAM_PER; ++k) {
+    const long long i = i0 + (long long)k * ADAM_THREADS;
+    if (i < a.n[q]) adam_elem(a, q, i, s_ns[q], s_bs[q]);
+  }
+  if (tid == 0) {
+    __threadfence();
+    s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (s_last && tid < a.np) {
+    a.step[tid][0] = t;
+    if (tid == 0) a.done[0] = 0u;
+  }
+}
+
+constexpr int FETCH_ROW = 16;
+__global__ void __launch_bounds__(64) step_fetch_kernel(const int* ring, int depth, int width, int* state,
+                                                        int* counter) {
+  const int i = threadIdx.x;
+  if (depth <= 64 && width <= FETCH_ROW) {
+    int v[FETCH_ROW];
+#pragma unroll
+    for (int e = 0; e < FETCH_ROW; ++e)
+      v[e] = (i < depth && e < width) ? __hip_atomic_load(ring + (size_t)i * width + e, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_SYSTEM)
+                                      : 0;
+    const int k = counter[0];
+    const int slot = k % depth;
+#pragma unroll
+    for (int e = 0; e < FETCH_ROW; ++e) {
+      const int t = __shfl(v[e], slot);
+      if (i == e && e < width) state[e] = t;
+    }
+    if (i == 0) counter[0] = k + 1;
+    return;
+  }
+  const int k = counter[0];
+  const int* row = ring + (size_t)(k % depth) * width;
+  if (i < width) state[i] = __hip_atomic_load(row + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (i == 0) counter[0] = k + 1;
+}
+
 }  // namespace thz
 
 using namespace thz;
@@ -492,5 +589,43 @@ extern "C" int thz_resample_backward(const thz_resample_desc* d, const void* gra
   hipLaunchKernelGGL(resample_bwd, dim3((n + 255) / 256), dim3(256), 0, s, (const float2*)grad_out,
                      (float2*)grad_in, a);
   THZ_LAUNCH_CHECK();
+  return THZ_OK;
+}
+
+extern "C" int thz_step_fetch(const int* ring, int depth, int width, int* state, int* counter, thz_stream_t stream) {
+  if (!ring || !state || !counter || depth < 1 || width < 1 || width > 64) return fail(THZ_E_ARG, "bad step-fetch arguments");
+  void* dring = nullptr;
+  THZ_HIP_CHECK(hipHostGetDevicePointer(&dring, const_cast<int*>(ring), 0));
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(step_fetch_kernel, dim3(1), dim3(64), 0, s, (const int*)dring, depth, width, state, counter);
+  THZ_LAUNCH_CHECK();
+  return THZ_OK;
+}
+
+extern "C" int thz_adam_step(const thz_adam_desc* d, const thz_adam_param* params, thz_stream_t stream) {
+  if (!d || !params || !d->done || d->nparams < 1 || d->nparams > THZ_MAX_ADAM_PARAMS)
+    return fail(THZ_E_ARG, "bad Adam arguments");
+  AdamArgs a{};
+  a.np = d->nparams;
+  a.lr = d->lr; a.b1 = d->beta1; a.b2 = d->beta2;
+  a.omb1 = (float)(1.0 - d->beta1); a.b2f = (float)d->beta2; a.omb2 = (float)(1.0 - d->beta2);
+  a.eps = (float)d->eps; a.wd = (float)d->weight_decay; a.decay = (float)(1.0 - d->lr * d->weight_decay);
+  a.decoupled = d->decoupled;
+  a.done = d->done;
+  long long blocks = 0;
+  for (int q = 0; q < a.np; ++q) {
+    const thz_adam_param& p = params[q];
+    if (!p.param || !p.grad || !p.exp_avg || !p.exp_avg_sq || !p.step || p.n < 1) return fail(THZ_E_ARG, "bad Adam parameter %d", q);
+    a.p[q] = p.param; a.g[q] = p.grad; a.m[q] = p.exp_avg; a.v[q] = p.exp_avg_sq; a.step[q] = p.step; a.n[q] = p.n;
+    a.blk0[q] = (int)blocks;
+    blocks += (p.n + ADAM_CHUNK - 1) / ADAM_CHUNK;
+    if (blocks > (1 << 30)) return fail(THZ_E_UNSUPPORTED, "Adam parameters too large");
+  }
+  a.blk0[a.np] = (int)blocks;
+  hipStream_t s = (hipStream_t)stream;
+  KernelTimer kt("adam_step", s);
+  hipLaunchKernelGGL(adam_step_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, s, a);
+  THZ_LAUNCH_CHECK();
+  kt.stop();
   return THZ_OK;
 }

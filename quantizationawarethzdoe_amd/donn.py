@@ -170,7 +170,7 @@ class DONNTrainer:
 
     def __init__(self, model, targets, lr=0.02, max_itrs=6000, group=None, graph=False, chained=True, loss_fn=None,
                  device_rng=True, capture_collective=False, force_collective=False):
-        from quantizationawarethzdoe_amd.qat import GradientAllReduce
+        from quantizationawarethzdoe_amd.qat import GradientAllReduce, _optimizer
         self.model = model
         self.targets = targets.to(model.device).float().contiguous()
         self.max_itrs = max_itrs
@@ -178,8 +178,7 @@ class DONNTrainer:
         self.chained = chained
         self.loss_fn = loss_fn
         self.params = [p for p in model.parameters() if p.requires_grad]
-        self.optimizer = torch.optim.Adam(self.params, lr=lr, capturable=graph,
-                                          fused=bool(self.params) and self.params[0].is_cuda)
+        self.optimizer = _optimizer("adam", self.params, lr, graph)
         self.allreduce = GradientAllReduce(self.params, group=group, force=force_collective)
         self.capture_collective = bool(capture_collective)  # qat.QATTrainer's option
         self._one = torch.ones((), dtype=torch.float32, device=model.device)
@@ -273,6 +272,7 @@ class DONNTrainer:
                 def whole():
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                        self._step_state.fetch()
                         loss = self._fb(su, st, frac)
                         self.allreduce.reduce()
                         self._opt()
@@ -284,6 +284,7 @@ class DONNTrainer:
                 self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
+                self._step_state.fetch()
                 loss = self._fb(su, st, frac)
             with torch.cuda.graph(g_opt, capture_error_mode=_CAPTURE_MODE):
                 self._opt()
@@ -303,11 +304,14 @@ class DONNTrainer:
         torch.index_select(self.targets, 0, labels, out=st)
         lead = self.model.does[0]
         phase = lead._graph_phase(frac)
-        self._step_state.upload(lead._dyn_values(frac), self.itr)
+        dyn = lead._dyn_values(frac)
         if phase not in self._graphs:
+            self._step_state.upload(dyn, self.itr)  # the capture's eager warm-up steps
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
+        self._step_state.stage(dyn, self.itr)
         g_fb.replay()
+        self._step_state.launched()
         if g_opt is not None:  # an eager collective between the two captured halves
             self.allreduce.reduce()
             g_opt.replay()

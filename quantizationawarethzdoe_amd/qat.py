@@ -261,34 +261,63 @@ class ExtendedDOFSystem(MultiPlaneSystem):
             p.z = c * mm + self.rand.uniform(lo * mm, hi * mm)
 
 
+def _optimizer(kind, params, lr, graph):
+    """Adam / AdamW: the one-launch HIP optimiser (optim.py) for device parameters, torch's otherwise."""
+    from quantizationawarethzdoe_amd import optim
+    if params and params[0].is_cuda:
+        return {"adam": optim.Adam, "adamw": optim.AdamW}[kind](params, lr=lr)
+    return {"adam": torch.optim.Adam, "adamw": torch.optim.AdamW}[kind](params, lr=lr, capturable=graph)
+
+
 class StepState:
     """The per-step device state of a graph-replayed trainer: int32 [5 + nz] = the float32 bits of
     the layer schedule (tau, s, beta), the device generator's (seed, step), then the float32 bits of
     the nz output-plane distances of a multi-plane system (``zdev``: the ASM kernels read them,
     thz_asm_desc.z_dev, so the extended-DOF planes can move every replay).
 
-    ``upload`` writes the host values into one slot of a pinned ring and enqueues an asynchronous
-    copy into the device state on the current stream: no pageable (synchronous) host->device copy
-    per step.  A slot is rewritten only after the copy that last read it has run (one event per
-    slot), so the host may run up to ``depth`` steps ahead of the GPU.
+    A replayed step gets its state with no host->device copy command: the host fills one slot of a
+    pinned ring (``stage``), and the graph's first node (``fetch``, thz_step_fetch, captured) copies
+    slot (device counter mod depth) into the state and advances the counter, so the replays of any
+    of the trainer's graphs run back to back.  ``launched`` (after each replay) counts the replays and
+    records an event after every ``EVERY``-th: a slot is rewritten only once an event recorded after
+    the replay that last read it has completed, so the host runs up to depth - EVERY steps ahead of
+    the GPU (an event between two replays costs the GPU ~5 us, a per-step one 8 % of a cfg4 step).
+    ``upload`` (an asynchronous copy from a second pinned ring) sets the state for the eager warm-up
+    steps before a capture.
 
     ``installed(layers)`` puts the state on the layers (``_dyn``; with device_rng also ``_rng``,
     two draw streams per layer) for the duration of a capture only: the captured kernels keep the
     pointers, while eager forwards after training draw from torch's generator and use their own
     iter_frac, as the reference's layers do."""
 
-    def __init__(self, device, seed, device_rng, depth=8, nz=0):
+    EVERY = 16
+
+    def __init__(self, device, seed, device_rng, depth=8, nz=0, ring=64):
         import numpy as np
-        self.state = torch.zeros(5 + nz, dtype=torch.int32, device=device)
+        self.width = 5 + nz
+        self.state = torch.zeros(self.width, dtype=torch.int32, device=device)
         self.dyn = self.state[:3].view(torch.float32)
         self.zdev = self.state[5:].view(torch.float32) if nz else None
+        self.counter = torch.zeros(1, dtype=torch.int32, device=device)
         self.seed = seed
         self.device_rng = device_rng
-        self._pinned = torch.zeros(depth, 5 + nz, dtype=torch.int32).pin_memory()
-        self._host = self._pinned.numpy()
         self._np = np
+        self._pinned = torch.zeros(depth, self.width, dtype=torch.int32).pin_memory()  # eager uploads
+        self._host = self._pinned.numpy()
         self._events = [None] * depth
         self._k = 0
+        assert ring % self.EVERY == 0 and ring >= 2 * self.EVERY
+        self._ring = torch.zeros(ring, self.width, dtype=torch.int32).pin_memory()  # replays (fetch)
+        self._ring_host = self._ring.numpy()
+        self._ring_events = [None] * (ring // self.EVERY)
+        self._fetches = 0  # replays staged so far == the device counter once they have run
+
+    def _fill(self, row, dyn, step, zs):
+        row[:3] = self._np.asarray(dyn, dtype=self._np.float32).view(self._np.int32)
+        row[3] = int(self.seed)
+        row[4] = int(step) & 0x7FFFFFFF
+        if zs is not None:
+            row[5:] = self._np.asarray(zs, dtype=self._np.float32).view(self._np.int32)
 
     def upload(self, dyn, step, zs=None):
         k = self._k
@@ -298,13 +327,33 @@ class StepState:
             ev = self._events[k] = torch.cuda.Event()
         else:
             ev.synchronize()
-        self._host[k, :3] = self._np.asarray(dyn, dtype=self._np.float32).view(self._np.int32)
-        self._host[k, 3] = int(self.seed)
-        self._host[k, 4] = int(step) & 0x7FFFFFFF
-        if zs is not None:
-            self._host[k, 5:] = self._np.asarray(zs, dtype=self._np.float32).view(self._np.int32)
+        self._fill(self._host[k], dyn, step, zs)
         self.state.copy_(self._pinned[k], non_blocking=True)
         ev.record()
+
+    def stage(self, dyn, step, zs=None):
+        """Fill the ring slot the next replay's fetch reads."""
+        f, n, ev = self._fetches, len(self._ring), self.EVERY
+        if f >= n:  # the slot's last reader is replay f - n: wait for the first event at or after it
+            c = -(-(f - n + 1) // ev) * ev
+            self._ring_events[(c // ev) % len(self._ring_events)].synchronize()
+        self._fill(self._ring_host[f % n], dyn, step, zs)
+
+    def launched(self):
+        """After a replay (whose graph fetched the staged slot): count it; every EVERY-th, an event."""
+        self._fetches += 1
+        if self._fetches % self.EVERY == 0:
+            i = (self._fetches // self.EVERY) % len(self._ring_events)
+            if self._ring_events[i] is None:
+                self._ring_events[i] = torch.cuda.Event()
+            self._ring_events[i].record()
+
+    def fetch(self):
+        """Captured as a step graph's first node: state <- ring[counter % depth], counter += 1."""
+        from quantizationawarethzdoe_amd import _lib
+        _lib.check(_lib.lib().thz_step_fetch(self._ring.data_ptr(), len(self._ring), self.width,
+                                             self.state.data_ptr(), self.counter.data_ptr(),
+                                             _prop._stream_handle()))
 
     @contextlib.contextmanager
     def installed(self, layers):
@@ -494,11 +543,11 @@ class QATTrainer:
         # loss(out_field_data, target): the fused HIP |E|^2 -> normalize -> MSE by default
         self.loss_fn = loss_fn or _optics.intensity_mse
         params = list(system.parameters())
-        # one fused Adam kernel per step on the GPU (torch's multi-tensor path launches ~7 small kernels).
-        # "adamw": the notebook's full-precision, naive-Gumbel and STE runs use torch.optim.AdamW with
-        # its defaults (weight_decay 0.01; experiment_four_focal_spots.ipynb cells 22, 33, 52)
-        opt = {"adam": torch.optim.Adam, "adamw": torch.optim.AdamW}[optimizer]
-        self.optimizer = opt(params, lr=lr, capturable=graph, fused=bool(params) and params[0].is_cuda)
+        # one Adam kernel per step on the GPU, the step counts advanced in it (optim.py; torch's fused
+        # capturable path launches a step-count kernel and an update kernel).  "adamw": the notebook's
+        # full-precision, naive-Gumbel and STE runs use torch.optim.AdamW with its defaults
+        # (weight_decay 0.01; experiment_four_focal_spots.ipynb cells 22, 33, 52)
+        self.optimizer = _optimizer(optimizer, params, lr, graph)
         self.allreduce = GradientAllReduce(list(system.parameters()), group=group, force=force_collective)
         self.capture_collective = bool(capture_collective)
         self._one = torch.ones((), dtype=torch.float32, device=system.device)
@@ -604,6 +653,7 @@ class QATTrainer:
                 def whole():
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, capture_error_mode=_CAPTURE_MODE):
+                        self._step_state.fetch()
                         loss = self._fb(frac)
                         self.allreduce.reduce()
                         self._opt()
@@ -615,6 +665,7 @@ class QATTrainer:
                 self.optimizer.zero_grad(set_to_none=True)
             g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_fb, capture_error_mode=_CAPTURE_MODE):
+                self._step_state.fetch()
                 loss = self._fb(frac)
             with torch.cuda.graph(g_opt, capture_error_mode=_CAPTURE_MODE):
                 self._opt()
@@ -622,12 +673,14 @@ class QATTrainer:
 
     def _graph_step(self, frac):
         phase = self.system.doe._graph_phase(frac)
-        self._step_state.upload(self.system.doe._dyn_values(frac), self.itr,
-                                self.system.planes if self.multi else None)
+        dyn, zs = self.system.doe._dyn_values(frac), (self.system.planes if self.multi else None)
         if phase not in self._graphs:
+            self._step_state.upload(dyn, self.itr, zs)  # the capture's eager warm-up steps
             self._graphs[phase] = self._capture(frac)
         g_fb, g_opt, loss = self._graphs[phase]
+        self._step_state.stage(dyn, self.itr, zs)
         g_fb.replay()
+        self._step_state.launched()
         if g_opt is not None:  # an eager collective between the two captured halves
             self.allreduce.reduce()
             g_opt.replay()

@@ -170,6 +170,13 @@ int main(void) {
   EXPECT(thz_radial_forward(NULL, 0, 0, 0, NULL, NULL) != THZ_OK, "radial bad");
   EXPECT(thz_radial_quant_backward(NULL, NULL, 0, 0, 0, NULL, NULL, NULL, NULL) != THZ_OK, "radial quant bad");
   EXPECT(thz_fft_rows(NULL, NULL, 0, 1024, 0, NULL) != THZ_OK, "fft rows bad");
+  int ring[4] = {0}, cnt = 0;
+  EXPECT(thz_step_fetch(NULL, 1, 1, NULL, NULL, NULL) != THZ_OK, "step fetch null");
+  EXPECT(thz_step_fetch(ring, 1, 65, ring, &cnt, NULL) != THZ_OK, "step fetch width > 64");
+  thz_adam_desc ad;
+  memset(&ad, 0, sizeof ad);
+  EXPECT(thz_adam_step(NULL, NULL, NULL) != THZ_OK, "adam null");
+  EXPECT(thz_adam_step(&ad, NULL, NULL) != THZ_OK, "adam no params");
   double ms = -1.0;
   long n = -1;
   EXPECT(thz_timing_reset() == THZ_OK && thz_timing_read("asm_cols", &ms, &n) == THZ_OK && n == 0,

@@ -5,6 +5,7 @@ all-reduce and the optimiser replay.  Same trajectory bit for bit as the split f
 sum is the identity), for the QAT (cfg4) and DONN (cfg5) trainers; the per-step times of both
 forms are printed (-s) for the record.  Multi-rank capture needs more than the one GPU a test box
 has; the eager split form stays the default."""
+import os
 import socket
 import time
 
@@ -26,6 +27,8 @@ def one_rank_rccl():
     import torch.distributed as dist
     if dist.is_initialized():
         pytest.skip("a process group is already initialised in this process")
+    # no event reuse in the PG watchdog (bench.py sets the same): see the note there
+    os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
                             device_id=torch.device("cuda:0"))
     try:

@@ -1,0 +1,63 @@
+"""The graph-replayed trainers' per-step state (qat.StepState, thz_step_fetch): each replay's first
+node copies the ring slot its host call staged into the device state, with no host->device copy
+command between replays.  Checked directly -- 3 x ring replays of two graphs sharing one state,
+alternated, the host running ahead of the GPU (no synchronisation between steps), every replay's
+state kept.  (The trainers' own graph-vs-eager tests cover it in use: test_optics_qat_gpu,
+test_qat_multi_gpu -- the extended-DOF planes move every step -- and test_donn_train_gpu.)"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a ROCm GPU")
+    return torch.device("cuda:0")
+
+
+def test_step_fetch_replays_read_their_own_slots():
+    from quantizationawarethzdoe_amd.qat import StepState
+    dev = _dev()
+    ss = StepState(dev, seed=1234, device_rng=True, nz=2, ring=32)
+    outs = [torch.zeros(ss.width, dtype=torch.int32, device=dev) for _ in range(2)]
+    graphs = []
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for o in outs:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                ss.fetch()
+                o.copy_(ss.state)
+            graphs.append(g)
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    kept, expect = [], []
+    for k in range(100):
+        dyn = [0.5 + k, 1.25 * k, -0.125 * k]
+        zs = [0.01 * k, 0.02 * k + 1.0]
+        ss.stage(dyn, 100 + k, zs)
+        graphs[k % 2].replay()
+        ss.launched()
+        kept.append(outs[k % 2].clone())
+        row = np.zeros(ss.width, dtype=np.int32)
+        ss._fill(row, dyn, 100 + k, zs)
+        expect.append(row)
+    torch.cuda.synchronize()
+    for k, (got, want) in enumerate(zip(kept, expect)):
+        assert np.array_equal(got.cpu().numpy(), want), k
+    assert int(ss.counter.item()) == 100
+    assert float(ss.dyn[0]) == 0.5 + 99 and float(ss.zdev[1]) == np.float32(0.02 * 99 + 1.0)
+
+
+def test_step_fetch_rejects_bad_arguments():
+    from quantizationawarethzdoe_amd import _lib
+    _dev()
+    st = torch.zeros(4, dtype=torch.int32, device="cuda:0")
+    ring = torch.zeros(4, dtype=torch.int32).pin_memory()
+    with pytest.raises(_lib.ThzError):
+        _lib.check(_lib.lib().thz_step_fetch(ring.data_ptr(), 1, 65, st.data_ptr(), st.data_ptr(), None))
+    with pytest.raises(_lib.ThzError):
+        _lib.check(_lib.lib().thz_step_fetch(None, 1, 4, st.data_ptr(), st.data_ptr(), None))
