@@ -314,6 +314,66 @@ __global__ void quant_fwd(QArgs a, const float* __restrict__ w, const float* __r
   for_mirrors(a, i, j, [&](int o) { hfull[o] = out; });
 }
 
+// The Gumbel kinds' forward with the L levels of a pixel on G adjacent lanes (G = the power of two
+// >= L): lane l forms level l's logit and Exp(1) draw -- the long part of the chain (score wraps,
+// draw, log) -- and the softmax runs on values gathered from the group in level order, so every
+// operation and its order is quant_fwd_px's while each lane's chain is about 1 / L as long.  quant_fwd's one-pixel-per-thread form ran 7.2 us at cfg4 (2,500 pixels,
+// 10 workgroups: a latency chain, not throughput).
+template <int G>
+__global__ void __launch_bounds__(256) quant_fwd_lv(QArgs a, const float* __restrict__ w,
+                                                    const float* __restrict__ expo, float* __restrict__ hfull,
+                                                    float* __restrict__ ysave) {
+  const QDyn q = get_dyn(a);
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int p = t / G, l = t % G;
+  const int n = a.hq * a.wq;
+  const int base = (int)(threadIdx.x & 63) - l;  // the group's first lane
+  const bool live = p < n && l < a.L;
+  const int pc = p < n ? p : n - 1, lc = l < a.L ? l : 0;  // in-range loads for the idle lanes
+  float logit, ex, hm = 0.f;
+  if (a.kind == THZ_Q_NGS) {
+    logit = w[(size_t)pc * a.L + lc];
+    ex = expo ? expo[(size_t)pc * a.L + lc] : rng_exp1(a.rng, a.rng_stream, (unsigned)(pc * a.L + lc));
+  } else {
+    float dsc, ph;
+    if (a.kind == THZ_Q_SGV1) {
+      ph = w[pc];
+    } else {
+      const float wc = fminf(fmaxf(w[pc], -a.clampv), a.clampv);
+      hm = a.hmax * sigm(wc);
+      ph = a.phase_scale * hm;
+    }
+    sgv3_score(a, q.s, ph, lc, &logit, &dsc);
+    ex = expo ? expo[(size_t)lc * n + pc] : rng_exp1(a.rng, a.rng_stream, (unsigned)(lc * n + pc));
+  }
+  // gumbel_soft over the group, in level order
+  const float yl = (logit + (-logf(ex))) / q.tau;
+  float mx = -INFINITY;
+  THZ_FOR_LEVELS(j, a.L) mx = fmaxf(mx, __shfl(yl, base + j));
+  const float el = expf(yl - mx);
+  float sum = 0.f;
+  THZ_FOR_LEVELS(j, a.L) sum += __shfl(el, base + j);
+  const float yv = el / sum;
+  float y[THZ_MAX_LUT];
+  int arg = 0;
+  float best = -1.f;
+  THZ_FOR_LEVELS(j, a.L) {
+    y[j] = __shfl(yv, base + j);
+    if (y[j] > best) {
+      best = y[j];
+      arg = j;
+    }
+  }
+  const float qv = st_value(a, y, arg);
+  float out = qv;
+  if (a.kind == THZ_Q_SGV3) out = a.iter_frac <= 0.8f ? (1.0f - q.beta) * hm + q.beta * qv : qv;
+  if (live && ysave) ysave[a.kind == THZ_Q_NGS ? (size_t)p * a.L + l : (size_t)l * n + p] = yv;
+  if (l == 0 && p < n) {
+    const int i = p / a.wq, jj = p - i * a.wq;
+    for_mirrors(a, i, jj, [&](int o) { hfull[o] = out; });
+  }
+}
+
 // dL/dw of quadrant pixel p from G = dL/dh summed over its mirror positions (the chain of
 // quant_fwd's pixel, reversed); NGS writes its L logits' gradients
 __device__ __forceinline__ void quant_bwd_px(const QArgs& a, const QDyn& q, const float* __restrict__ w,
@@ -549,7 +609,16 @@ extern "C" int thz_quant_forward(const thz_quant_desc* d, const float* weight, c
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("quant_fwd", s);
   const int n = d->hq * d->wq;
-  hipLaunchKernelGGL(quant_fwd, dim3((n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+  if (gumbel && a.L > 1) {  // the levels on adjacent lanes
+    if (a.L <= 4)
+      hipLaunchKernelGGL(quant_fwd_lv<4>, dim3((4 * n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+    else if (a.L <= 8)
+      hipLaunchKernelGGL(quant_fwd_lv<8>, dim3((8 * n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+    else
+      hipLaunchKernelGGL(quant_fwd_lv<16>, dim3((16 * n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+  } else {
+    hipLaunchKernelGGL(quant_fwd, dim3((n + 255) / 256), dim3(256), 0, s, a, weight, noise_exp, height_full, y_soft);
+  }
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;
