@@ -305,7 +305,8 @@ static bool loss_args(const thz_loss_desc* d, LossArgs* a) {
 // (pinned host memory, never cached), the counter advanced by lane 0.  Rings of <= 64 slots of
 // <= 16 values: lane l reads slot l's row beside the counter load (one round trip to host memory
 // instead of two in sequence), the counter's slot is broadcast from its lane.
-constexpr int ADAM_THREADS = 256, ADAM_PER = 1, ADAM_CHUNK = ADAM_THREADS * ADAM_PER;
+constexpr int ADAM_THREADS = 256;
+constexpr long long ADAM_PER4_FROM = 16384;  // elements: 4 per thread from here (fewer workgroups, fences)
 struct AdamArgs {
   float* p[THZ_MAX_ADAM_PARAMS];
   const float* g[THZ_MAX_ADAM_PARAMS];
@@ -335,10 +336,12 @@ __device__ __forceinline__ void adam_elem(const AdamArgs& a, int q, long long i,
   a.p[q][i] = p + nstep * (m / (sqrtf(v) / bc2s + a.eps));
 }
 
-// A workgroup is ADAM_CHUNK elements of one parameter (one per thread: a one-workgroup loop over a
-// 2,500-element map ran 2-3x longer, its loads in sequence).  Thread q < np reads parameter q's step
+// A workgroup is PER x 256 elements of one parameter: one per thread for the QAT maps (a
+// one-workgroup loop over a 2,500-element map ran 2-3x longer, its loads in sequence), four for
+// larger sets (the DONN's 30,000: 30 workgroups instead of 118, each with its release fence).  Thread q < np reads parameter q's step
 // count and forms its scalars (fp64 bias corrections); the last workgroup to finish advances the
 // counts, after every workgroup has read them.
+template <int PER>
 __global__ void __launch_bounds__(ADAM_THREADS) adam_step_kernel(AdamArgs a) {
   __shared__ float s_ns[THZ_MAX_ADAM_PARAMS], s_bs[THZ_MAX_ADAM_PARAMS];
   __shared__ int s_last;
@@ -354,9 +357,9 @@ __global__ void __launch_bounds__(ADAM_THREADS) adam_step_kernel(AdamArgs a) {
   const int bid = blockIdx.x;
   int q = 0;
   while (q + 1 < a.np && bid >= a.blk0[q + 1]) ++q;
-  const long long i0 = (long long)(bid - a.blk0[q]) * ADAM_CHUNK + tid;
+  const long long i0 = (long long)(bid - a.blk0[q]) * (PER * ADAM_THREADS) + tid;
 #pragma unroll
-  for (int k = 0; k < ADAM_PER; ++k) {
+  for (int k = 0; k < PER; ++k) {
     const long long i = i0 + (long long)k * ADAM_THREADS;
     if (i < a.n[q]) adam_elem(a, q, i, s_ns[q], s_bs[q]);
   }
@@ -612,19 +615,23 @@ extern "C" int thz_adam_step(const thz_adam_desc* d, const thz_adam_param* param
   a.eps = (float)d->eps; a.wd = (float)d->weight_decay; a.decay = (float)(1.0 - d->lr * d->weight_decay);
   a.decoupled = d->decoupled;
   a.done = d->done;
+  long long total = 0;
+  for (int q = 0; q < a.np; ++q) total += params[q].n;
+  const int per = total >= ADAM_PER4_FROM ? 4 : 1, chunk = per * ADAM_THREADS;
   long long blocks = 0;
   for (int q = 0; q < a.np; ++q) {
     const thz_adam_param& p = params[q];
     if (!p.param || !p.grad || !p.exp_avg || !p.exp_avg_sq || !p.step || p.n < 1) return fail(THZ_E_ARG, "bad Adam parameter %d", q);
     a.p[q] = p.param; a.g[q] = p.grad; a.m[q] = p.exp_avg; a.v[q] = p.exp_avg_sq; a.step[q] = p.step; a.n[q] = p.n;
     a.blk0[q] = (int)blocks;
-    blocks += (p.n + ADAM_CHUNK - 1) / ADAM_CHUNK;
+    blocks += (p.n + chunk - 1) / chunk;
     if (blocks > (1 << 30)) return fail(THZ_E_UNSUPPORTED, "Adam parameters too large");
   }
   a.blk0[a.np] = (int)blocks;
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("adam_step", s);
-  hipLaunchKernelGGL(adam_step_kernel, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, s, a);
+  if (per == 4) hipLaunchKernelGGL(adam_step_kernel<4>, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, s, a);
+  else hipLaunchKernelGGL(adam_step_kernel<1>, dim3((unsigned)blocks), dim3(ADAM_THREADS), 0, s, a);
   THZ_LAUNCH_CHECK();
   kt.stop();
   return THZ_OK;

@@ -2,7 +2,8 @@
 (the reference notebooks' optimisers, single-tensor form) over 60 steps of seeded gradients:
 parameters and both moments within fp32 rounding (the kernel evaluates torch's expressions in the
 same fp32 order; the bias corrections' rounding differs at most), step counts exact; several
-parameters of ragged sizes in one launch (chunks of 256, a 1-element parameter), more parameters than one launch takes (split launches), L2 and decoupled weight decay,
+parameters of ragged sizes in one launch (chunks of 1,024 above 16,384 elements, of 256 below; a
+1-element parameter), more parameters than one launch takes (split launches), L2 and decoupled weight decay,
 and the step captured in a HIP graph and replayed (the step counts advance on the device)."""
 import pytest
 import torch
@@ -24,7 +25,7 @@ def _params(sizes, dev, g):
 
 
 @pytest.mark.parametrize("kind,wd", [("adam", 0.0), ("adam", 0.05), ("adamw", None), ("adamw", 0.1)])
-@pytest.mark.parametrize("sizes", [SIZES, [(20,)] * 19], ids=["ragged", "split"])
+@pytest.mark.parametrize("sizes", [SIZES, SIZES + [(100, 100)], [(20,)] * 19], ids=["ragged", "large", "split"])
 def test_adam_matches_torch(kind, wd, sizes):
     from quantizationawarethzdoe_amd import optim
     dev = _dev()
