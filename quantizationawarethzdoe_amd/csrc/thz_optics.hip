@@ -148,13 +148,16 @@ __global__ void __launch_bounds__(FIN_THREADS) loss_finish_kernel(LossSink ls) {
     ls.stats[3 * b + 0] = m;
     ls.stats[3 * b + 1] = __int_as_float((int)(0xffffffffu - (unsigned)acc.key));
     ls.stats[3 * b + 2] = (float)(acc.ii / md - acc.it);
-    ls.terms()[b] = acc.ii / (md * md) - 2.0 * acc.it / md + acc.tt;
-    __threadfence();
+    // the term written through to memory (an agent-scope atomic store) and its completion awaited
+    // before the arrival is counted: the release the last workgroup needs, without the L2
+    // write-back of an agent-scope fence (which every one of B workgroups would pay)
+    __hip_atomic_store(ls.terms() + b, acc.ii / (md * md) - 2.0 * acc.it / md + acc.tt, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
     s_last = atomicAdd(ls.counter(), 1ull) == (unsigned long long)(ls.B - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   double part = 0.0;  // B terms in order: thread t sums a contiguous run
   const int per = (ls.B + FIN_THREADS - 1) / FIN_THREADS;
   for (int q = threadIdx.x * per; q < min(ls.B, (threadIdx.x + 1) * per); ++q)
@@ -363,10 +366,9 @@ __global__ void __launch_bounds__(ADAM_THREADS) adam_step_kernel(AdamArgs a) {
     const long long i = i0 + (long long)k * ADAM_THREADS;
     if (i < a.n[q]) adam_elem(a, q, i, s_ns[q], s_bs[q]);
   }
-  if (tid == 0) {
-    __threadfence();
-    s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;
-  }
+  // no release fence: nothing this workgroup wrote is read by the last one, and its step-count read
+  // (thread q, above) has returned before the arrival is counted (the count's value is already used)
+  if (tid == 0) s_last = atomicAdd(a.done, 1u) == gridDim.x - 1;
   __syncthreads();
   if (s_last && tid < a.np) {
     a.step[tid][0] = t;
