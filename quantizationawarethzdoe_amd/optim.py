@@ -44,6 +44,15 @@ class _ThzAdamBase(torch.optim.Optimizer):
             st["step"] = torch.zeros((), dtype=torch.float32, device=p.device)
             st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        else:
+            # a loaded state_dict (e.g. torch.optim.Adam's, whose non-capturable step count stays on
+            # the host): the kernel reads every state tensor on the parameter's device, fp32, dense
+            for k in ("step", "exp_avg", "exp_avg_sq"):
+                v = st[k]
+                if not torch.is_tensor(v):
+                    v = torch.tensor(float(v))
+                if v.device != p.device or v.dtype != torch.float32 or not v.is_contiguous():
+                    st[k] = v.to(device=p.device, dtype=torch.float32).contiguous()
         return st
 
     @torch.no_grad()

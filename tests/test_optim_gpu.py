@@ -5,6 +5,8 @@ same fp32 order; the bias corrections' rounding differs at most), step counts ex
 parameters of ragged sizes in one launch (chunks of 1,024 above 16,384 elements, of 256 below; a
 1-element parameter), more parameters than one launch takes (split launches), L2 and decoupled weight decay,
 and the step captured in a HIP graph and replayed (the step counts advance on the device)."""
+import copy
+
 import pytest
 import torch
 
@@ -87,3 +89,32 @@ def test_adam_refuses_what_it_does_not_implement():
         optim.Adam([p]).step()
     with pytest.raises(ValueError):
         optim.Adam([p], amsgrad=True)
+
+
+def test_adam_continues_from_a_torch_state_dict():
+    """A torch.optim.Adam state (its step count on the host) loaded into the HIP Adam: the kernel
+    gets device copies and the run continues as torch's own would."""
+    from quantizationawarethzdoe_amd import optim
+    dev = _dev()
+    g = torch.Generator().manual_seed(9)
+    a = _params([(50, 50), (7,)], dev, g)
+    b = [p.detach().clone().requires_grad_(True) for p in a]
+    ref = torch.optim.Adam(b, lr=0.02, foreach=False)
+    for _ in range(5):
+        for q in b:
+            q.grad = torch.randn(q.shape, generator=g).to(dev)
+        ref.step()
+    with torch.no_grad():
+        for p, q in zip(a, b):
+            p.copy_(q)
+    ours = optim.Adam(a, lr=0.02)
+    ours.load_state_dict(copy.deepcopy(ref.state_dict()))  # (loading shares tensors already in place)
+    for _ in range(10):
+        grads = [torch.randn(p.shape, generator=g).to(dev) for p in a]
+        for p, q, gr in zip(a, b, grads):
+            p.grad, q.grad = gr.clone(), gr.clone()
+        ours.step()
+        ref.step()
+    for p, q in zip(a, b):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=2e-5, atol=2e-6)
+        assert float(ours.state[p]["step"]) == 15.0 and ours.state[p]["step"].device == p.device
