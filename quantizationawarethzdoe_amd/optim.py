@@ -67,8 +67,12 @@ class _ThzAdamBase(torch.optim.Optimizer):
                 if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()
                         and not p.grad.is_sparse and p.grad.dtype == torch.float32):
                     raise ValueError("thz Adam: contiguous fp32 device parameters and gradients only")
-            for k in range(0, len(ps), _lib.THZ_MAX_ADAM_PARAMS):
-                self._launch(group, ps[k:k + _lib.THZ_MAX_ADAM_PARAMS])
+            by_dev = {}
+            for p in ps:  # one launch reads one device's memory
+                by_dev.setdefault(p.device, []).append(p)
+            for dps in by_dev.values():
+                for k in range(0, len(dps), _lib.THZ_MAX_ADAM_PARAMS):
+                    self._launch(group, dps[k:k + _lib.THZ_MAX_ADAM_PARAMS])
         return loss
 
     def _launch(self, group, ps):
