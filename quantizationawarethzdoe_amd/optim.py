@@ -28,9 +28,10 @@ class _ThzAdamBase(torch.optim.Optimizer):
     _decoupled = False
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0, amsgrad=False,
-                 maximize=False, **unused):
-        if amsgrad or maximize:
-            raise ValueError("thz Adam: amsgrad / maximize are not supported")
+                 maximize=False, foreach=None, fused=None, capturable=None, differentiable=False):
+        # foreach / fused / capturable: torch's implementation choices, all the same one launch here
+        if amsgrad or maximize or differentiable:
+            raise ValueError("thz Adam: amsgrad / maximize / differentiable are not supported")
         if not 0.0 <= lr or not 0.0 <= eps or not 0.0 <= weight_decay:
             raise ValueError(f"invalid lr / eps / weight_decay: {lr}, {eps}, {weight_decay}")
         if not (0.0 <= betas[0] < 1.0 and 0.0 <= betas[1] < 1.0):

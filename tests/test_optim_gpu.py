@@ -89,6 +89,11 @@ def test_adam_refuses_what_it_does_not_implement():
         optim.Adam([p]).step()
     with pytest.raises(ValueError):
         optim.Adam([p], amsgrad=True)
+    with pytest.raises(ValueError):
+        optim.AdamW([p], differentiable=True)
+    with pytest.raises(TypeError):
+        optim.Adam([p], nesterov=True)  # not an Adam argument
+    optim.Adam([torch.zeros(2, device=dev, requires_grad=True)], foreach=True, fused=True, capturable=True)
 
 
 def test_adam_continues_from_a_torch_state_dict():
