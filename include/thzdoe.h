@@ -452,7 +452,7 @@ int thz_fft64_rows(const void* in, void* out, int rows, int n, int inverse, thz_
  * the fetches so far.  Copies slot (counter mod depth) into state (device [width] int32) and
  * increments counter -- a step's graph captures it as its first node, so every replay reads the
  * slot its host call filled without a host->device copy command between replays.  The caller
- * rewrites a slot only after the replay that read it has run.  1 <= width <= 64.
+ * rewrites a slot only after the replay that read it has run.  1 <= width <= 5 + THZ_MAX_Z.
  */
 int thz_step_fetch(const int* ring, int depth, int width, int* state, int* counter, thz_stream_t stream);
 

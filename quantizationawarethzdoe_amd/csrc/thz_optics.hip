@@ -399,7 +399,7 @@ __global__ void __launch_bounds__(64) step_fetch_kernel(const int* ring, int dep
   }
   const int k = counter[0];
   const int* row = ring + (size_t)(k % depth) * width;
-  if (i < width) state[i] = __hip_atomic_load(row + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int e = i; e < width; e += 64) state[e] = __hip_atomic_load(row + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   if (i == 0) counter[0] = k + 1;
 }
 
@@ -598,7 +598,8 @@ extern "C" int thz_resample_backward(const thz_resample_desc* d, const void* gra
 }
 
 extern "C" int thz_step_fetch(const int* ring, int depth, int width, int* state, int* counter, thz_stream_t stream) {
-  if (!ring || !state || !counter || depth < 1 || width < 1 || width > 64) return fail(THZ_E_ARG, "bad step-fetch arguments");
+  if (!ring || !state || !counter || depth < 1 || width < 1 || width > 5 + THZ_MAX_Z)
+    return fail(THZ_E_ARG, "bad step-fetch arguments");
   void* dring = nullptr;
   THZ_HIP_CHECK(hipHostGetDevicePointer(&dring, const_cast<int*>(ring), 0));
   hipStream_t s = (hipStream_t)stream;

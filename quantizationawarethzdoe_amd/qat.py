@@ -280,7 +280,7 @@ class StepState:
     slot (device counter mod depth) into the state and advances the counter, so the replays of any
     of the trainer's graphs run back to back.  ``launched`` (after each replay) counts the replays and
     records an event after every ``EVERY``-th: a slot is rewritten only once an event recorded after
-    the replay that last read it has completed, so the host runs up to depth - EVERY steps ahead of
+    the replay that last read it has completed, so the host runs up to ring - EVERY steps ahead of
     the GPU (an event between two replays costs the GPU ~5 us, a per-step one 8 % of a cfg4 step).
     ``upload`` (an asynchronous copy from a second pinned ring) sets the state for the eager warm-up
     steps before a capture.

@@ -172,7 +172,7 @@ int main(void) {
   EXPECT(thz_fft_rows(NULL, NULL, 0, 1024, 0, NULL) != THZ_OK, "fft rows bad");
   int ring[4] = {0}, cnt = 0;
   EXPECT(thz_step_fetch(NULL, 1, 1, NULL, NULL, NULL) != THZ_OK, "step fetch null");
-  EXPECT(thz_step_fetch(ring, 1, 65, ring, &cnt, NULL) != THZ_OK, "step fetch width > 64");
+  EXPECT(thz_step_fetch(ring, 1, 6 + THZ_MAX_Z, ring, &cnt, NULL) != THZ_OK, "step fetch width > 5 + THZ_MAX_Z");
   thz_adam_desc ad;
   memset(&ad, 0, sizeof ad);
   EXPECT(thz_adam_step(NULL, NULL, NULL) != THZ_OK, "adam null");

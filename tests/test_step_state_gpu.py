@@ -58,6 +58,31 @@ def test_step_fetch_rejects_bad_arguments():
     st = torch.zeros(4, dtype=torch.int32, device="cuda:0")
     ring = torch.zeros(4, dtype=torch.int32).pin_memory()
     with pytest.raises(_lib.ThzError):
-        _lib.check(_lib.lib().thz_step_fetch(ring.data_ptr(), 1, 65, st.data_ptr(), st.data_ptr(), None))
+        _lib.check(_lib.lib().thz_step_fetch(ring.data_ptr(), 1, 6 + 256, st.data_ptr(), st.data_ptr(), None))
     with pytest.raises(_lib.ThzError):
         _lib.check(_lib.lib().thz_step_fetch(None, 1, 4, st.data_ptr(), st.data_ptr(), None))
+
+
+def test_step_fetch_wide_state():
+    """A multi-plane state wider than one wave (5 + 100 planes): the general path's strided copy."""
+    from quantizationawarethzdoe_amd.qat import StepState
+    dev = _dev()
+    ss = StepState(dev, seed=5, device_rng=False, nz=100, ring=32)
+    out = torch.zeros(ss.width, dtype=torch.int32, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ss.fetch()
+            out.copy_(ss.state)
+    torch.cuda.current_stream().wait_stream(side)
+    for k in range(40):
+        zs = [0.001 * (k + j) for j in range(100)]
+        ss.stage([1.0, 2.0, 3.0], k, zs)
+        g.replay()
+        ss.launched()
+    torch.cuda.synchronize()
+    row = np.zeros(ss.width, dtype=np.int32)
+    ss._fill(row, [1.0, 2.0, 3.0], 39, [0.001 * (39 + j) for j in range(100)])
+    assert np.array_equal(out.cpu().numpy(), row)
