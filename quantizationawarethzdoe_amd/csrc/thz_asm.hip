@@ -1254,60 +1254,6 @@ static size_t ws_bytes(const AsmGeom& g) {
          tab_bytes(g);
 }
 
-// The adjoint of a Z-plane forward (sum over planes): per z-chunk, K1 over the chunk's input
-// planes and the Z-summing K2 (adding into U after the first chunk); then K3 once.
-static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
-                           hipStream_t s, FftPlan pw, FftPlan ph, bool mx_tabs) {
-  a.zsum = 1;
-  a.tab_blocks = 0;
-  a.kfull = g.ncols * g.BC;  // every column task runs all of its chunk's planes
-  a.kparts = 1;
-  const int th = threads_for(g.Ph);
-  for (int z0 = 0; z0 < Z; z0 += g.zc) {
-    a.zoff = z0;
-    a.nz = std::min(g.zc, Z - z0);
-    a.zacc = z0 > 0;
-    {
-      KernelTimer kt("asm_rows_fwd", s);
-      if (k1_mid(g.Pw, a)) {
-        hipLaunchKernelGGL((asm_rows_fwd<Mx300::N, true>), dim3(a.nz * g.BC * g.Hin), dim3(MX_T), fft_lds_bytes_io(g.Pw),
-                           s, (const float2*)in, T, pw, a);
-      } else {
-        THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(a.nz * g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in,
-                        T, pw, a);
-      }
-      THZ_LAUNCH_CHECK();
-      kt.stop();
-    }
-    {
-      KernelTimer kt("asm_cols", s);
-      if (mx_kind(g.Ph) == Mx300::N) {
-        if (mx_tabs) {
-          hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
-          THZ_LAUNCH_CHECK();
-        }
-        const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
-        hipLaunchKernelGGL(asm_cols_mx_zsum<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
-      } else {
-        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
-        THZ_POW2_SWITCH(g.Ph, asm_cols_zsum, dim3(a.kfull), dim3(th), lds2, s, (const float2*)T, U, ph, a);
-      }
-      THZ_LAUNCH_CHECK();
-      kt.stop();
-    }
-  }
-  a.zoff = 0;
-  a.nz = 1;
-  {
-    KernelTimer kt("asm_rows_inv", s);
-    THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
-                    (float2*)out, pw, a);
-    THZ_LAUNCH_CHECK();
-    kt.stop();
-  }
-  return THZ_OK;
-}
-
 // The 300-point column pass's tables (sqrt(k^2 - K^2) per element, the kept band per plane) depend
 // only on the geometry, the wavelengths and the planes, so for host-given planes in one z-chunk
 // they are kept per device across calls: the first call (not under stream capture) forms them
@@ -1369,6 +1315,72 @@ static TabEntry* tab_cache_get(const AsmArgs& a, const AsmGeom& g, int Z, hipStr
 static void tab_cache_formed(TabEntry* e, hipStream_t s) {
   std::lock_guard<std::mutex> lk(g_tab_mu);
   (void)hipEventRecord(e->ev, s);
+}
+
+// The adjoint of a Z-plane forward (sum over planes): per z-chunk, K1 over the chunk's input
+// planes and the Z-summing K2 (adding into U after the first chunk); then K3 once.
+static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
+                           hipStream_t s, FftPlan pw, FftPlan ph, bool mx_tabs) {
+  a.zsum = 1;
+  a.tab_blocks = 0;
+  a.kfull = g.ncols * g.BC;  // every column task runs all of its chunk's planes
+  a.kparts = 1;
+  const int th = threads_for(g.Ph);
+  // one z-chunk of host planes: the column tables from the per-device cache (no tables launch
+  // once they are ready)
+  TabEntry* tce = nullptr;
+  bool tform = false;
+  if (mx_tabs && !a.zdev && Z <= g.zc) {
+    tce = tab_cache_get(a, g, Z, s, &tform);
+    if (tce) {
+      a.sqt = tce->sq;
+      a.mzt = tce->mz;
+    }
+  }
+  for (int z0 = 0; z0 < Z; z0 += g.zc) {
+    a.zoff = z0;
+    a.nz = std::min(g.zc, Z - z0);
+    a.zacc = z0 > 0;
+    {
+      KernelTimer kt("asm_rows_fwd", s);
+      if (k1_mid(g.Pw, a)) {
+        hipLaunchKernelGGL((asm_rows_fwd<Mx300::N, true>), dim3(a.nz * g.BC * g.Hin), dim3(MX_T), fft_lds_bytes_io(g.Pw),
+                           s, (const float2*)in, T, pw, a);
+      } else {
+        THZ_ROWS_SWITCH(g.Pw, asm_rows_fwd, dim3(a.nz * g.BC * g.Hin), fft_lds_bytes_io(g.Pw), s, (const float2*)in,
+                        T, pw, a);
+      }
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+    {
+      KernelTimer kt("asm_cols", s);
+      if (mx_kind(g.Ph) == Mx300::N) {
+        if (mx_tabs && !(tce && !tform)) {
+          hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
+          THZ_LAUNCH_CHECK();
+          if (tform) tab_cache_formed(tce, s);
+        }
+        const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
+        hipLaunchKernelGGL(asm_cols_mx_zsum<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+      } else {
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        THZ_POW2_SWITCH(g.Ph, asm_cols_zsum, dim3(a.kfull), dim3(th), lds2, s, (const float2*)T, U, ph, a);
+      }
+      THZ_LAUNCH_CHECK();
+      kt.stop();
+    }
+  }
+  a.zoff = 0;
+  a.nz = 1;
+  {
+    KernelTimer kt("asm_rows_inv", s);
+    THZ_ROWS_SWITCH(g.Pw, asm_rows_inv, dim3(g.BC * g.Hout), fft_lds_bytes_io(g.Pw), s, (const float2*)U,
+                    (float2*)out, pw, a);
+    THZ_LAUNCH_CHECK();
+    kt.stop();
+  }
+  return THZ_OK;
 }
 
 // K1 once, then (K2, K3) per z-chunk, on a prepared argument block.
