@@ -24,7 +24,6 @@
 #include <mutex>
 #include <cmath>
 #include <cstdlib>
-#include <cstring>
 #include <tuple>
 #include <vector>
 
@@ -1254,69 +1253,6 @@ static size_t ws_bytes(const AsmGeom& g) {
          tab_bytes(g);
 }
 
-// The 300-point column pass's tables (sqrt(k^2 - K^2) per element, the kept band per plane) depend
-// only on the geometry, the wavelengths and the planes, so for host-given planes in one z-chunk
-// they are kept per device across calls: the first call (not under stream capture) forms them
-// into a library buffer as usual and records an event; once a later call finds that event done
-// the tables are reused and K1 drops its table workgroups (cfg4 -2 %, batch-32 DONN -2.5 %,
-// profiles/r05_experiments.txt 19).  A call under capture uses only tables already known ready.
-struct TabEntry {
-  float* sq = nullptr;
-  int* mz = nullptr;
-  hipEvent_t ev = nullptr;
-  bool ready = false;
-};
-static std::mutex g_tab_mu;
-static std::map<std::vector<unsigned>, TabEntry> g_tab_cache;
-constexpr size_t TAB_CACHE_MAX = 256;  // entries; buffers are never freed (captured graphs keep them)
-
-static std::vector<unsigned> tab_key(const AsmArgs& a, const AsmGeom& g, int Z) {
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  auto fb = [](float f) { unsigned u; std::memcpy(&u, &f, 4); return u; };
-  std::vector<unsigned> k = {(unsigned)dev, (unsigned)g.Ph, (unsigned)g.Pw, (unsigned)g.ncols, (unsigned)g.J,
-                             (unsigned)g.C, (unsigned)a.bl, (unsigned)Z, fb(a.dx), fb(a.dy)};
-  for (int c = 0; c < g.C; ++c) k.push_back(fb(a.lam[c]));
-  for (int z = 0; z < Z; ++z) k.push_back(fb(a.zv[z]));
-  return k;
-}
-
-// the cached tables for this call, or null (form them in the workspace as before); *form: the
-// entry's tables are to be formed by this call (then tab_cache_formed after its K1)
-static TabEntry* tab_cache_get(const AsmArgs& a, const AsmGeom& g, int Z, hipStream_t s, bool* form) {
-  *form = false;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cs) != hipSuccess) return nullptr;
-  const bool capturing = cs != hipStreamCaptureStatusNone;
-  std::lock_guard<std::mutex> lk(g_tab_mu);
-  const std::vector<unsigned> key = tab_key(a, g, Z);
-  auto it = g_tab_cache.find(key);
-  if (it == g_tab_cache.end()) {
-    if (capturing || g_tab_cache.size() >= TAB_CACHE_MAX) return nullptr;
-    TabEntry e;
-    const size_t sqb = (size_t)g.C * g.ncols * g.Ph * sizeof(float), mzb = (size_t)g.C * g.ncols * Z * sizeof(int);
-    if (hipMalloc(&e.sq, sqb) != hipSuccess) return nullptr;
-    if (hipMalloc(&e.mz, mzb) != hipSuccess || hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) {
-      (void)hipFree(e.sq);
-      return nullptr;
-    }
-    it = g_tab_cache.emplace(key, e).first;
-    *form = true;
-    return &it->second;
-  }
-  TabEntry& e = it->second;
-  if (!e.ready && !capturing && hipEventQuery(e.ev) == hipSuccess) e.ready = true;
-  if (e.ready) return &e;
-  if (capturing) return nullptr;
-  *form = true;  // formed again (the first forming has not finished): same values, stream-ordered
-  return &e;
-}
-
-static void tab_cache_formed(TabEntry* e, hipStream_t s) {
-  std::lock_guard<std::mutex> lk(g_tab_mu);
-  (void)hipEventRecord(e->ev, s);
-}
-
 // The adjoint of a Z-plane forward (sum over planes): per z-chunk, K1 over the chunk's input
 // planes and the Z-summing K2 (adding into U after the first chunk); then K3 once.
 static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
@@ -1326,17 +1262,6 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
   a.kfull = g.ncols * g.BC;  // every column task runs all of its chunk's planes
   a.kparts = 1;
   const int th = threads_for(g.Ph);
-  // one z-chunk of host planes: the column tables from the per-device cache (no tables launch
-  // once they are ready)
-  TabEntry* tce = nullptr;
-  bool tform = false;
-  if (mx_tabs && !a.zdev && Z <= g.zc) {
-    tce = tab_cache_get(a, g, Z, s, &tform);
-    if (tce) {
-      a.sqt = tce->sq;
-      a.mzt = tce->mz;
-    }
-  }
   for (int z0 = 0; z0 < Z; z0 += g.zc) {
     a.zoff = z0;
     a.nz = std::min(g.zc, Z - z0);
@@ -1356,10 +1281,9 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
     {
       KernelTimer kt("asm_cols", s);
       if (mx_kind(g.Ph) == Mx300::N) {
-        if (mx_tabs && !(tce && !tform)) {
+        if (mx_tabs) {
           hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
           THZ_LAUNCH_CHECK();
-          if (tform) tab_cache_formed(tce, s);
         }
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
         hipLaunchKernelGGL(asm_cols_mx_zsum<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
@@ -1396,19 +1320,8 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     a.mzt = (int*)(tabs + tab_sq_bytes(g));
   }
   if (g.adj && Z > 1) return run_adjoint_sum(a, g, Z, in, out, T, U, s, pw, ph, mx_tabs);
-  // square mixed-radix grids (cfg4 / cfg5): the first z-chunk's column tables ride along with K1,
-  // or come from the per-device cache (host planes, one z-chunk)
+  // square mixed-radix grids (cfg4 / cfg5): the first z-chunk's column tables ride along with K1
   a.tab_blocks = mx_tabs && mx_kind(g.Pw) == Mx300::N ? g.C * g.ncols : 0;
-  TabEntry* tce = nullptr;
-  bool tform = false;
-  if (a.tab_blocks && !a.zdev && Z <= g.zc) {
-    tce = tab_cache_get(a, g, Z, s, &tform);
-    if (tce) {
-      a.sqt = tce->sq;
-      a.mzt = tce->mz;
-      if (!tform) a.tab_blocks = 0;
-    }
-  }
   {
     KernelTimer kt("asm_rows_fwd", s);
     a.zoff = 0;
@@ -1421,7 +1334,6 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
                       (const float2*)in, T, pw, a);
     }
     THZ_LAUNCH_CHECK();
-    if (tform) tab_cache_formed(tce, s);
     kt.stop();
   }
   for (int z0 = 0; z0 < Z; z0 += g.zc) {
@@ -1430,7 +1342,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     {
       KernelTimer kt("asm_cols", s);
       if (mx_kind(g.Ph) == Mx300::N) {
-        if (mx_tabs && !(z0 == 0 && (a.tab_blocks || tce))) {
+        if (mx_tabs && !(z0 == 0 && a.tab_blocks)) {
           hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
           THZ_LAUNCH_CHECK();
         }
