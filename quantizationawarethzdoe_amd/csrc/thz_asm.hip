@@ -58,6 +58,9 @@ struct AsmArgs {
   // into one spectrum per column and inverts once (zacc: add into U, for the chunks after the
   // first), K3 runs once on the single summed plane
   int zsum, zacc;
+  // 1: the power-of-two column pass may take the plane recurrence where its planes allow it
+  // (asm_cols_body decides per column; 0 = THZ_K2_RECURRENCE=0, the per-plane sincos everywhere)
+  int zrec;
   float dx, dy, scale;
   const float2* tft;  // RSC: column-major transfer-function table [C][ncols][Ph] (nullptr: analytic ASM)
   int vec;            // VRS: plane b == 2 is Ez = (Ex x + Ey y) / r computed in the row pass
@@ -350,6 +353,23 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // ---------------------------------------------------------------------------------------------
 // K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
 // ---------------------------------------------------------------------------------------------
+// Plane zz (> 0) of the column task's range [z_lo, z_hi) may be reached by the plane recurrence of
+// asm_cols_body: with dz = z_1 - z_0 of the range, the step z_zz - z_{zz-1} and eps = step - dz are
+// both EXACT fp32 differences (so the recurrence's phase sums to (z_zz - z_0) sq exactly) and
+// |eps| k <= 1e-4 rad (so 1 + i eps sq stands for exp(i eps sq) to 5e-9).  Evaluated on the device,
+// so a device-resident plane list (thz_asm_desc.z_dev) decides exactly as the same host list does.
+// register slot of the step factor D of kept spectrum value r (r < 4 or r >= 12): the slots
+// [4, 12) of sp, whose values are zero whenever the recurrence runs
+__host__ __device__ constexpr int rec_dslot(int r) { return r < 4 ? r + 4 : r - 4; }
+
+__device__ __forceinline__ bool recurrence_step_ok(const AsmArgs& a, int z_lo, int zz, float kl) {
+  const float z0 = zval(a, a.zoff + z_lo), z1 = zval(a, a.zoff + z_lo + 1);
+  const float zp = zval(a, a.zoff + z_lo + zz - 1), zc = zval(a, a.zoff + z_lo + zz);
+  const float dz = z1 - z0, step = zc - zp, eps = step - dz;
+  return dz != 0.0f && (double)dz == (double)z1 - (double)z0 && (double)step == (double)zc - (double)zp &&
+         (double)eps == (double)step - (double)dz && fabs((double)eps) * (double)kl <= 1e-4;
+}
+
 // ZSUM: the Z-summing adjoint's column pass (a separate instantiation, so the forward's register
 // allocation is untouched by it).
 template <int PN, bool ZSUM>
@@ -428,6 +448,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     const float kl2 = tf_mul(kl, kl);
     const float Ky2 = tf_mul(Ky, Ky);
     // strided over the chunk: a z_chunk may exceed the workgroup (64 threads at P = 1024)
+    int* zok = mz + THZ_MAX_Z;  // plane recurrence allowed at this plane (below)
     for (int zz = tid; zz < z_hi - z_lo; zz += nt) {
       const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + z_lo + zz));
       int lo = -1, hi = PN / 2 + 1;
@@ -442,6 +463,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         }
       }
       mz[zz] = lo;
+      if constexpr (!ZSUM) zok[zz] = zz == 0 || recurrence_step_ok(a, z_lo, zz, kl);
     }
     // sqrt(k^2 - Kx^2 - Ky^2) of the elements this thread holds: z-independent, computed once
     // per column (the per-z work is then one product and one sincos per element)
@@ -454,6 +476,18 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         sq[m][r] = sqrtf(fmaxf(tf_sub(kl2, tf_add(tf_mul(Kx, Kx), Ky2)), 0.0f));
       }
     __syncthreads();  // mz visible
+    // the plane recurrence (below) for this column?
+    bool rec = false;
+    if constexpr (!ZSUM && RL == 16 && MBL == 1) {
+      if (a.zrec && z_hi - z_lo >= 3) {
+        int mmax = -1, ok = 1;
+        for (int q = 0; q < z_hi - z_lo; ++q) {
+          mmax = max(mmax, mz[q]);
+          ok &= zok[q];
+        }
+        rec = __builtin_amdgcn_readfirstlane(ok) && __builtin_amdgcn_readfirstlane(mmax) < PN / 4;
+      }
+    }
     if constexpr (ZSUM) {
       // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
 #pragma unroll
@@ -494,9 +528,56 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       fft_pow2_io<true, PN, TT, FFT_TAIL, false, false>(lds, twl, tz, ld1, sv1);
       return;
     }
+    // Plane recurrence (a uniform z-sweep such as cfg2's linspace): instead of one sincos per
+    // element per plane, G_j = sp H_{z_j} advances by one complex product per plane,
+    //   G_j = G_{j-1} D (1 + i eps_j sq),   D = exp(i dz sq),   eps_j = (z_j - z_{j-1}) - dz,
+    // which tracks the given fp32 planes exactly: recurrence_step_ok has checked that every
+    // difference is exact in fp32 and |eps_j| k <= 1e-4 rad, so 1 + i theta stands for
+    // exp(i theta) to 5e-9.  D is formed in double and rounded once (<= 6e-8 per plane, 4e-6
+    // over 64 planes); the chunk's first plane is the sincos form's value bit for bit.
+    // Taken when the column keeps no row with |m_x| >= PN/4 on any plane of the chunk: the
+    // inverse's first-stage operands r in [4, 12) are then zero, and the registers of those 8
+    // spectrum values hold the 8 step factors D (sp[0][rec_dslot(r)]); sq holds +-sq.  Both forms
+    // share one z-loop and one inverse transform on the same registers (as two regions the
+    // structurizer kept one form's live-ins live through the other and spilled).
+    constexpr bool REC = !ZSUM && RL == 16 && MBL == 1;
+    float dz = 0.f, zprev = 0.f;
+    if constexpr (REC) {
+      if (rec) {
+        const float z0 = zval(a, a.zoff + z_lo);
+        dz = zval(a, a.zoff + z_lo + 1) - z0;
+        zprev = z0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          if (r >= 4 && r < 12) continue;
+          float sn, cs;
+          sincos_hw(tf_mul(z0, sq[0][r]), &sn, &cs);
+          sp[0][r] = cmul(sp[0][r], make_float2(cs, a.adjoint ? -sn : sn));
+          const float2 d = cis_dd((double)dz * (double)sq[0][r]);
+          sp[0][rec_dslot(r)] = make_float2(d.x, a.adjoint ? -d.y : d.y);
+          if (a.adjoint) sq[0][r] = -sq[0][r];
+          // one element's double-precision evaluation at a time (all eight interleaved need more
+          // registers than the kernel has)
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
     for (int zz = z_lo; zz < z_hi; ++zz) {
       const float z = zval(a, a.zoff + zz);
       const int M = mz[zz - z_lo];
+      if constexpr (REC) {
+        if (rec && zz > z_lo) {
+          const float eps = tf_sub(tf_sub(z, zprev), dz);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (r >= 4 && r < 12) continue;
+            const float2 g = cmul(sp[0][r], sp[0][rec_dslot(r)]);
+            const float th = eps * sq[0][r];
+            sp[0][r] = make_float2(fmaf(-th, g.y, g.x), fmaf(th, g.x, g.y));
+          }
+        }
+        zprev = z;
+      }
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
@@ -504,9 +585,17 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       // the first stage's operands r in [4, 12) are the rows PN/4 <= |m_x| < 3 PN/4: when this
       // plane's kept band M is below PN/4 (all but the few columns near m_y = 0 at cfg2) they are
       // zero for every thread, and a scalar branch skips their sincos and product
-      const bool mid0 = __builtin_amdgcn_readfirstlane(M) < PN / 4;
+      const int Ms = __builtin_amdgcn_readfirstlane(M);
+      const bool mid0 = Ms < PN / 4;
       auto ld1 = [&](int m, int r, int idx) {
         if (RL == 16 && r >= 4 && r < 12 && mid0) return make_float2(0.f, 0.f);
+        if constexpr (REC) {
+          if (rec) {
+            // element tz + r PN/16: m_x = tz + r PN/16 (r < 4), tz + r PN/16 - PN (r >= 12)
+            const bool keep = r < 4 ? tz <= Ms - r * (PN / 16) : tz >= PN - r * (PN / 16) - Ms;
+            return keep ? sp[0][r] : make_float2(0.f, 0.f);
+          }
+        }
         const int mx = freq_index(idx, PN);
         if (mx > M || -mx > M) return make_float2(0.f, 0.f);
         float sn, cs;
@@ -1153,7 +1242,7 @@ static int ensure_lds_attr() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
-    const int mx = (int)fft_lds_bytes(FFT_MAX_N) + 4 * THZ_MAX_Z;
+    const int mx = (int)fft_lds_bytes(FFT_MAX_N) + 8 * THZ_MAX_Z;
     std::vector<const void*> ks;
     add_kernels<0>(ks);
     add_kernels<1024>(ks);
@@ -1307,6 +1396,13 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
   return THZ_OK;
 }
 
+// THZ_K2_RECURRENCE=0 keeps the per-plane sincos everywhere (the A/B and parity tests compare the
+// two forms; read per call so a test can toggle it)
+static bool plane_recurrence_disabled() {
+  const char* v = std::getenv("THZ_K2_RECURRENCE");
+  return v && v[0] == '0';
+}
+
 // K1 once, then (K2, K3) per z-chunk, on a prepared argument block.
 static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void* out, float2* T, float2* U,
                         hipStream_t s, FftPlan pw, FftPlan ph, char* tabs = nullptr) {
@@ -1355,8 +1451,9 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         else
           hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
       } else {
-        const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 8 * THZ_MAX_Z;  // mz and zok
         const int ntask = k2_tasks(g, &a, th, lds2);
+        a.zrec = !plane_recurrence_disabled();
         THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
       }
       THZ_LAUNCH_CHECK();

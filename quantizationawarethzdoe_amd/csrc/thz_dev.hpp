@@ -91,6 +91,41 @@ __device__ __forceinline__ float2 cis_d(double ph) {
   return make_float2(cs, sn);
 }
 
+// exp(i ph) for a phase in double, evaluated in double and rounded to fp32 once per component
+// (error <= 6e-8 per component): the per-plane step factor of the column pass's plane recurrence,
+// whose phase error accumulates over the planes of a chunk.  Quadrant reduction by a two-part pi/2,
+// Taylor polynomials on [-pi/4, pi/4] (truncation < 5e-17).
+__device__ __forceinline__ float2 cis_dd(double ph) {
+  const double q = rint(ph * 0.63661977236758134308);
+  double r = fma(-q, 1.5707963267948966192, ph);
+  r = fma(-q, 6.1232339957367658e-17, r);
+  const double r2 = r * r;
+  // sin r = r + r^3 ps(r^2), ps = -1/3! + r^2/5! - r^4/7! + ... - r^12/15!
+  double ps = -1.0 / 1307674368000.0;
+  ps = fma(r2, ps, 1.0 / 6227020800.0);
+  ps = fma(r2, ps, -1.0 / 39916800.0);
+  ps = fma(r2, ps, 1.0 / 362880.0);
+  ps = fma(r2, ps, -1.0 / 5040.0);
+  ps = fma(r2, ps, 1.0 / 120.0);
+  ps = fma(r2, ps, -1.0 / 6.0);
+  const double s = fma(r * r2, ps, r);
+  double pc = 1.0 / 20922789888000.0;  // 1/16!
+  pc = fma(r2, pc, -1.0 / 87178291200.0);
+  pc = fma(r2, pc, 1.0 / 479001600.0);
+  pc = fma(r2, pc, -1.0 / 3628800.0);
+  pc = fma(r2, pc, 1.0 / 40320.0);
+  pc = fma(r2, pc, -1.0 / 720.0);
+  pc = fma(r2, pc, 1.0 / 24.0);
+  pc = fma(r2, pc, -0.5);
+  const double c = fma(r2, pc, 1.0);
+  const int iq = (int)q;
+  double sn = (iq & 1) ? c : s;
+  double cs = (iq & 1) ? s : c;
+  if (iq & 2) sn = -sn;
+  if ((iq + 1) & 2) cs = -cs;
+  return make_float2((float)cs, (float)sn);
+}
+
 __device__ __forceinline__ int freq_index(int i, int n) { return i < n - n / 2 ? i : i - n; }
 
 // Aperture masks (Components/Aperture.py:44-136): the aperture kernel and the ASM window mask
