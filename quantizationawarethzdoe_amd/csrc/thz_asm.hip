@@ -189,11 +189,15 @@ struct Geo {
 // Compile-time mixed-radix sizes (MxPlan, one 64-thread workgroup per transform): the P = 300
 // grid of the cfg4 / cfg5 layers.  Other non-power-of-two sizes run the runtime plan.
 constexpr int MX_T = 64;
+// threads of a compile-time mixed-radix transform: one wave for 300 (the radix-5 stages' 60
+// butterflies on one lane each), two waves for 500 (its radix-5 stages' 100 and radix-4 stage's 125
+// butterflies one per lane: on one wave, two per lane, the row and column passes spilled)
+__host__ __device__ constexpr int mx_threads(int n) { return n == 500 ? 128 : MX_T; }
 // waves per SIMD of the mixed-radix column pass: 6 lets it keep its 70 VGPRs (8 spilled 5 of them
 // to scratch): cfg5 chained batch 256 0.986 -> 0.952 ms, dual-plane 0.080 -> 0.077 ms per step,
 // batch 32 0.290 -> 0.296 (profiles/r05_experiments.txt 4)
 constexpr int MX_WPE = 6;
-__host__ __device__ constexpr bool is_mx(int n) { return n == Mx300::N; }
+__host__ __device__ constexpr bool is_mx(int n) { return n == Mx300::N || n == Mx500::N; }
 
 __device__ __forceinline__ int band_col(int j, int P, int J, int ncols) {
   const int c = freq_index(j, P) + J;
@@ -211,7 +215,7 @@ __device__ __forceinline__ float2 vrs_ez(float2 ex, float2 ey, float x, float y,
 #pragma clang fp contract(on)
 
 template <int PN>
-__device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq);
+__device__ __forceinline__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq);
 // The K1 input element s of row h of plane `plane` (s < Win): the field, or what the fused
 // loaders make of it -- the loss gradient of the adjoint of the fused loss, the DOE modulation
 // t_c(h + noise) (writing the noisy height map once), or the VRS Ez plane.
@@ -294,9 +298,11 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
   extern __shared__ float2 lds[];
   const int tid = threadIdx.x, nt = blockDim.x;
   const int nrows = gridDim.x - a.tab_blocks;
-  if constexpr (is_mx(PN)) {
+  if constexpr (PN == Mx300::N) {
     // the extra workgroups past the rows: the mixed-radix column pass's tables of the first
-    // z-chunk (asm_tf_tables, one launch fewer; K2 runs after this kernel on the stream)
+    // z-chunk (asm_tf_tables, one launch fewer; K2 runs after this kernel on the stream).  The
+    // 300-point pass only: in asm_rows_fwd<500> the tables' code made the compiler copy the whole
+    // argument block to scratch (1.6 KB per lane); P = 500 launches asm_tf_tables<500> instead
     if ((int)blockIdx.x >= nrows) {
       tf_tables_body<PN>(a, blockIdx.x - nrows, 1);
       return;
@@ -324,8 +330,10 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
     };
     fft_pow2_run<false, PN, TT, FFT_ROWS>(lds, twl, tid, ld, sv, tw_hook);
   } else if constexpr (is_mx(PN)) {
-    if constexpr (MID) __builtin_assume(tid >= 0 && tid < MX_T);
-    const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
+    constexpr int MT = mx_threads(PN);
+    if constexpr (MID) __builtin_assume(tid >= 0 && tid < MT);
+    using MP = typename MxOf<PN>::type;
+    const auto twr = MP::template twiddles<MT>(pw.tw, tid);
     auto ld = [&](int, int, int idx) {
       const int s = idx - (MID ? PN / 3 : a.in_c0);
       return (s >= 0 && s < (MID ? PN / 3 : a.Win)) ? fetch(s) : make_float2(0.f, 0.f);
@@ -334,7 +342,7 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
       const int c = band_col(j, PN, a.J, a.ncols);
       if (c >= 0) dst[blk(c, h, a.Hin)] = v;
     };
-    Mx300::run<false, MX_T>(lds, twr, tid, ld, sv);
+    MP::template run<false, MT>(lds, twr, tid, ld, sv);
   } else {
     for (int j = tid; j < a.Pw; j += nt) {
       const int s = j - a.in_c0;
@@ -703,7 +711,7 @@ __global__ void __launch_bounds__(1024) asm_cols_zsum(const float2* __restrict__
 // chunk (bisection with the exact reference-order tests, one lane per z; see asm_cols).  Every
 // plane of the wavelength shares them, so the column pass does no fp32 division.
 template <int PN>
-__device__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq) {
+__device__ __forceinline__ void tf_tables_body(const AsmArgs& a, int blk, int with_sq) {
   const int li = blk / a.ncols, c = blk - li * a.ncols;
   const float lam = a.lam[li];
   const float Ky = kfreq(c - a.J, a.Pw, a.dy);
@@ -763,7 +771,7 @@ __global__ void __launch_bounds__(MX_T) asm_tf_tables(AsmArgs a, int with_sq) {
 template <class MP, bool ZSUM, bool MID = false>
 __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph,
                                                  AsmArgs a) {
-  constexpr int PN = MP::N, RL = MP::RL, NBL = PN / RL, MBL = (NBL + MX_T - 1) / MX_T;
+  constexpr int PN = MP::N, RL = MP::RL, MT = mx_threads(PN), NBL = PN / RL, MBL = (NBL + MT - 1) / MT;
   static_assert(MP::R0 == RL, "the inverse must start where the forward ends");
   extern __shared__ float2 lds[];
   int id, z_lo = 0, z_hi = a.nz;
@@ -779,14 +787,14 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
   const float2* col = T + (size_t)bc * a.ncb * CB * a.Hin + blk(c, 0, a.Hin);
   int tid = threadIdx.x;
   float2 sp[MBL][RL];
-  if constexpr (MID) __builtin_assume(tid >= 0 && tid < MX_T);
+  if constexpr (MID) __builtin_assume(tid >= 0 && tid < MT);
   auto ld0 = [&](int, int, int idx) {
     const int s = idx - (MID ? PN / 3 : a.in_r0);
     return (s >= 0 && s < (MID ? PN / 3 : a.Hin)) ? col[(size_t)s * CB] : make_float2(0.f, 0.f);
   };
   auto sv0 = [&](int m, int r, int, float2 v) { sp[m][r] = v; };
-  const auto twr = MP::template twiddles<MX_T>(ph.tw, tid);
-  if constexpr (!ZSUM) MP::template run<false, MX_T>(lds, twr, tid, ld0, sv0);
+  const auto twr = MP::template twiddles<MT>(ph.tw, tid);
+  if constexpr (!ZSUM) MP::template run<false, MT>(lds, twr, tid, ld0, sv0);
   if (!ZSUM && a.tft) {  // RSC: tabulated transfer function FFT2(K), one z
     const float2* tcol = a.tft + ((size_t)(bc % a.C) * a.ncols + c) * PN;
     int tz = threadIdx.x;
@@ -800,7 +808,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
       const int r = j - a.out_r0;
       if (r >= 0 && r < a.Hout) dst[u_roff(r)] = cscale(v, a.scale);
     };
-    MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
+    MP::template run<true, MT>(lds, twr, tz, ld1, sv1);
     return;
   }
   // kept rows |m_x| <= M_z per z and the z-independent sqrt(k^2 - K^2) of the elements this
@@ -811,9 +819,9 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
   float sq[MBL][RL];
 #pragma unroll
   for (int m = 0; m < MBL; ++m) {
-    const int i = tid + m * MX_T;
+    const int i = tid + m * MT;
 #pragma unroll
-    for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MX_T == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
+    for (int r = 0; r < RL; ++r) sq[m][r] = (NBL % MT == 0 || i < NBL) ? sqc[i + r * NBL] : 0.f;
   }
   if constexpr (ZSUM) {
     // adjoint over the chunk's planes: sp = sum_z FFT(T_z column) conj(H_z), then one inverse
@@ -838,7 +846,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
         sincos_hw(tf_mul(z, sq[m][r]), &sn, &cs);
         sp[m][r] = cadd(sp[m][r], cmul(v, make_float2(cs, -sn)));
       };
-      MP::template run<false, MX_T>(lds, twr, tz, ldz, acc);
+      MP::template run<false, MT>(lds, twr, tz, ldz, acc);
     }
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
@@ -851,7 +859,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
         dst[u_roff(r)] = a.zacc ? cadd(dst[u_roff(r)], o) : o;
       }
     };
-    MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
+    MP::template run<true, MT>(lds, twr, tz, ld1, sv1);
     return;
   }
   for (int zz = z_lo; zz < z_hi; ++zz) {
@@ -859,7 +867,7 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
     const int M = mzc[zz];
     int tz = threadIdx.x;
     asm volatile("" : "+v"(tz));
-    if constexpr (MID) __builtin_assume(tz >= 0 && tz < MX_T);
+    if constexpr (MID) __builtin_assume(tz >= 0 && tz < MT);
     auto ld1 = [&](int m, int r, int idx) {
       const int mx = freq_index(idx, PN);
       if (mx > M || -mx > M) return make_float2(0.f, 0.f);
@@ -872,24 +880,24 @@ __device__ __forceinline__ void asm_cols_mx_body(const float2* __restrict__ T, f
       const int r = j - (MID ? PN / 3 : a.out_r0);
       if ((unsigned)r < (unsigned)(MID ? PN / 3 : a.Hout)) dst[u_roff(r)] = cscale(v, a.scale);
     };
-    MP::template run<true, MX_T>(lds, twr, tz, ld1, sv1);
+    MP::template run<true, MT>(lds, twr, tz, ld1, sv1);
   }
 }
 
 template <class MP>
-__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx(
+__global__ void __launch_bounds__(mx_threads(MP::N)) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx(
     const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_mx_body<MP, false>(T, U, ph, a);
 }
 
 template <class MP>
-__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_mid(
+__global__ void __launch_bounds__(mx_threads(MP::N)) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_mid(
     const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_mx_body<MP, false, true>(T, U, ph, a);
 }
 
 template <class MP>
-__global__ void __launch_bounds__(MX_T) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_zsum(
+__global__ void __launch_bounds__(mx_threads(MP::N)) __attribute__((amdgpu_waves_per_eu(MX_WPE))) asm_cols_mx_zsum(
     const float2* __restrict__ T, float2* __restrict__ U, FftPlan ph, AsmArgs a) {
   asm_cols_mx_body<MP, true>(T, U, ph, a);
 }
@@ -937,8 +945,10 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
     if constexpr (LOSS) acc.add(v, trow[w], ibase + (unsigned)w);
   };
   if constexpr (is_mx(PN)) {
-    if constexpr (MID) __builtin_assume(tid >= 0 && tid < MX_T);
-    const auto twr = Mx300::twiddles<MX_T>(pw.tw, tid);
+    constexpr int MT = mx_threads(PN);
+    if constexpr (MID) __builtin_assume(tid >= 0 && tid < MT);
+    using MP = typename MxOf<PN>::type;
+    const auto twr = MP::template twiddles<MT>(pw.tw, tid);
     auto ld = [&](int, int, int j) {
       const int c = band_col(j, PN, a.J, a.ncols);
       return c >= 0 ? src[blk_u(c, r, a.Hout)] : make_float2(0.f, 0.f);
@@ -948,7 +958,7 @@ __device__ __forceinline__ void rows_inv_body(const float2* __restrict__ U, floa
       const int w = j - (MID ? PN / 3 : a.out_c0);
       if ((unsigned)w < (unsigned)(MID ? PN / 3 : a.Wout)) put(w, v);
     };
-    Mx300::run<true, MX_T>(lds, twr, tid, ld, sv);
+    MP::template run<true, MT>(lds, twr, tid, ld, sv);
   } else if constexpr (PN > 0) {
     // The twiddle tables' global loads go out first and their LDS writes happen after the first
     // stage's gather (the hook runs before the first exchange), so the gather does not wait behind
@@ -1268,7 +1278,15 @@ static int mx_kind(int n) { return is_mx(n) ? n : 0; }
 // K1 / K3: the mixed-radix instantiation or the power-of-two switch
 #define THZ_ROWS_SWITCH(n, KER, G, LDSB, ...)                                                      \
   if (mx_kind(n) == Mx300::N) hipLaunchKernelGGL(KER<Mx300::N>, G, dim3(MX_T), LDSB, __VA_ARGS__); \
+  else if (mx_kind(n) == Mx500::N) hipLaunchKernelGGL(KER<Mx500::N>, G, dim3(mx_threads(500)), LDSB, __VA_ARGS__); \
   else THZ_POW2_SWITCH(n, KER, G, dim3(threads_for(n)), LDSB, __VA_ARGS__)
+// the mixed-radix column-pass kernels (asm_cols_mx*, templated on the plan) and their tables
+#define THZ_MX_COLS(n, KER, ...)                                                                   \
+  if ((n) == Mx300::N) hipLaunchKernelGGL(KER<Mx300>, __VA_ARGS__);                               \
+  else hipLaunchKernelGGL(KER<Mx500>, __VA_ARGS__)
+#define THZ_MX_TABLES(n, ...)                                                                      \
+  if ((n) == Mx300::N) hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, __VA_ARGS__);                  \
+  else hipLaunchKernelGGL(asm_tf_tables<Mx500::N>, __VA_ARGS__)
 
 // The 300-point passes with the layers' windows ([N/3, 2N/3) in and out: padding 2 with unpad,
 // cfg4 / cfg5) as compile-time constants: the column pass (asm_cols_mx_mid: 80.8 vs 83.3 us per
@@ -1305,6 +1323,7 @@ static int k2_resident(int Ph, int threads, size_t lds) {
     default: k = (const void*)asm_cols<0>; break;
   }
   if (mx_kind(Ph) == Mx300::N) k = (const void*)asm_cols_mx<Mx300>;
+  if (mx_kind(Ph) == Mx500::N) k = (const void*)asm_cols_mx<Mx500>;
   int per_cu = 0, cus = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds) != hipSuccess ||
       hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -1369,13 +1388,13 @@ static int run_adjoint_sum(AsmArgs a, const AsmGeom& g, int Z, const void* in, v
     }
     {
       KernelTimer kt("asm_cols", s);
-      if (mx_kind(g.Ph) == Mx300::N) {
+      if (mx_kind(g.Ph)) {
         if (mx_tabs) {
-          hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
+          THZ_MX_TABLES(g.Ph, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
           THZ_LAUNCH_CHECK();
         }
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
-        hipLaunchKernelGGL(asm_cols_mx_zsum<Mx300>, dim3(a.kfull), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+        THZ_MX_COLS(g.Ph, asm_cols_mx_zsum, dim3(a.kfull), dim3(mx_threads(g.Ph)), lds2, s, (const float2*)T, U, ph, a);
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 4 * THZ_MAX_Z;
         THZ_POW2_SWITCH(g.Ph, asm_cols_zsum, dim3(a.kfull), dim3(th), lds2, s, (const float2*)T, U, ph, a);
@@ -1409,15 +1428,16 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
   int e;
   if ((e = ensure_lds_attr())) return e;
   const int th = threads_for(g.Ph);
-  const bool mx_tabs = mx_kind(g.Ph) == Mx300::N && !a.tft;
+  const bool mx_tabs = mx_kind(g.Ph) && !a.tft;
   if (mx_tabs) {
     if (!tabs) return fail(THZ_E_WORKSPACE, "mixed-radix column tables need workspace");
     a.sqt = (float*)tabs;
     a.mzt = (int*)(tabs + tab_sq_bytes(g));
   }
   if (g.adj && Z > 1) return run_adjoint_sum(a, g, Z, in, out, T, U, s, pw, ph, mx_tabs);
-  // square mixed-radix grids (cfg4 / cfg5): the first z-chunk's column tables ride along with K1
-  a.tab_blocks = mx_tabs && mx_kind(g.Pw) == Mx300::N ? g.C * g.ncols : 0;
+  // square 300-point grids (cfg4 / cfg5): the first z-chunk's column tables ride along with K1
+  // (tf_tables_body<PN> of K1's own size: Ph == Pw)
+  a.tab_blocks = mx_tabs && g.Pw == g.Ph && g.Pw == Mx300::N ? g.C * g.ncols : 0;
   {
     KernelTimer kt("asm_rows_fwd", s);
     a.zoff = 0;
@@ -1437,19 +1457,19 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
     a.nz = std::min(g.zc, Z - z0);
     {
       KernelTimer kt("asm_cols", s);
-      if (mx_kind(g.Ph) == Mx300::N) {
+      if (mx_kind(g.Ph)) {
         if (mx_tabs && !(z0 == 0 && a.tab_blocks)) {
-          hipLaunchKernelGGL(asm_tf_tables<Mx300::N>, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
+          THZ_MX_TABLES(g.Ph, dim3(g.C * g.ncols), dim3(MX_T), 0, s, a, z0 == 0);
           THZ_LAUNCH_CHECK();
         }
       }
-      if (mx_kind(g.Ph) == Mx300::N) {
+      if (mx_kind(g.Ph)) {
         const size_t lds2 = lds_floats2(g.Ph) * sizeof(float2) + 4 * THZ_MAX_Z;
-        const int ntask = k2_tasks(g, &a, MX_T, lds2);
-        if (mx_mid(a))
+        const int ntask = k2_tasks(g, &a, mx_threads(g.Ph), lds2);
+        if (g.Ph == Mx300::N && mx_mid(a))
           hipLaunchKernelGGL(asm_cols_mx_mid<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
         else
-          hipLaunchKernelGGL(asm_cols_mx<Mx300>, dim3(ntask), dim3(MX_T), lds2, s, (const float2*)T, U, ph, a);
+          THZ_MX_COLS(g.Ph, asm_cols_mx, dim3(ntask), dim3(mx_threads(g.Ph)), lds2, s, (const float2*)T, U, ph, a);
       } else {
         const size_t lds2 = fft_lds_bytes(g.Ph) + 8 * THZ_MAX_Z;  // mz and zok
         const int ntask = k2_tasks(g, &a, th, lds2);

@@ -1007,6 +1007,20 @@ struct MxPlan {
 // so the forward's spectrum is 5 values per lane and the inverse starts from it directly
 // (5 4 3 5 and 5 12 5 measured within noise / slower)
 using Mx300 = MxPlan<5, 3, 4, 5>;
+// 500 = 5 4 5 5 (the extended-DOF grid: 100 x 100 with padding scale 4): first and last radix 5
+// (100 butterflies: two per lane of the 64-thread workgroup, the second on 36 lanes)
+using Mx500 = MxPlan<5, 4, 5, 5>;
+// the compile-time plan of a mixed-radix size
+template <int N>
+struct MxOf;
+template <>
+struct MxOf<300> {
+  using type = Mx300;
+};
+template <>
+struct MxOf<500> {
+  using type = Mx500;
+};
 
 // Full transform of one row held in LDS (natural order in and out).  Unnormalised.
 template <bool INV>

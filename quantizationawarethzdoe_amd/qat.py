@@ -18,6 +18,7 @@ MI355X mapping
 from __future__ import annotations
 
 import contextlib
+import os
 import time
 
 import torch
@@ -403,20 +404,37 @@ def release_step_graph(modules):
                     pend.quant = None
 
 
+def collective_capture_safe():
+    """Whether an RCCL collective may be captured into a step graph in this process: only with
+    ``TORCH_NCCL_CUDA_EVENT_CACHE=0``.  With torch's default (cached, reused CUDA events) the process
+    group's watchdog was seen to abort the process, about once in ten runs, querying an event "last
+    recorded in a capturing stream" after a captured all-reduce.  The variable is read
+    by ProcessGroupNCCL when the group is created, so the library cannot set it for the caller: it
+    must be in the environment before ``init_process_group``; the trainers check it when they
+    capture and otherwise keep the collective out of the graph (``agreed_capture``)."""
+    return os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") == "0"
+
+
 def agreed_capture(allreduce, capture_fn):
     """Capture the whole step with the collective inside it (``capture_fn() -> (graph, loss)``),
     with every rank agreeing on the outcome: after the attempt, an eager all_reduce(MIN) of a
     success flag outside any capture.  Returns capture_fn's result, or None when the capture failed
     on ANY rank -- every rank then discards its graph and builds the split form (fwd/bwd graph, eager
     all-reduce, optimiser graph), so no rank replays a graph with a captured collective while
-    another runs the eager one.  Without an active collective a capture error is raised as is."""
+    another runs the eager one.  A rank whose environment does not make the capture safe
+    (``collective_capture_safe``) does not attempt it and votes for the split form.  Without an
+    active collective a capture error is raised as is."""
     ok, res, err = 1, None, None
-    try:
-        res = capture_fn()
-    except RuntimeError as e:
-        if not allreduce.active:
-            raise
-        ok, err = 0, e
+    if allreduce.active and allreduce.capturable and not collective_capture_safe():
+        ok, err = 0, RuntimeError("TORCH_NCCL_CUDA_EVENT_CACHE is not 0 in this process (set it before "
+                                  "init_process_group to capture the all-reduce)")
+    else:
+        try:
+            res = capture_fn()
+        except RuntimeError as e:
+            if not allreduce.active:
+                raise
+            ok, err = 0, e
     if allreduce.active:
         flag = torch.tensor([ok], dtype=torch.int32, device=allreduce.flat.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=allreduce.group)

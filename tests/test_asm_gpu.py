@@ -355,6 +355,41 @@ def test_asm_p300_mixed_radix_vs_oracle(zs, bl, H, W):
     assert abs(complex(lhs - rhs)) / abs(complex(lhs)) <= 1e-4
 
 
+@pytest.mark.parametrize("zs,bl", [([0.05, 0.06, 0.07, 0.08, 0.09], "exact"), ([0.052], "exact"),
+                                   ([0.03, 0.11, -0.04], "approx")], ids=["edof_5z", "1z", "3z_approx"])
+def test_asm_p500_compile_time_plan_vs_oracle(zs, bl):
+    """P = 500 (the extended-DOF grid: 100 x 100, padding scale 4) on the compile-time mixed-radix
+    plan 5 4 5 5 (Mx500: two-wave transforms in K1, K2, the Z-summing K2 and K3) vs the fp64
+    oracle, every plane at <= max(1e-4, 1.5 x the fp32 oracle's own error); plus the adjoint
+    identity <A x, y> = <x, A^H y> of the Z-plane forward and its one-launch Z-summing adjoint."""
+    EF, ASM = _prop_cls()
+    dev = _dev()
+    rng = np.random.default_rng(50)
+    x = (rng.standard_normal((2, 1, 100, 100)) + 1j * rng.standard_normal((2, 1, 100, 100))).astype(np.complex64)
+    wl = C0 / 300e9
+    field = EF(torch.from_numpy(x).to(dev), wavelengths=wl, spacing=[1e-3, 1e-3], device=dev)
+    prop = ASM(z_distance=zs[0], padding_scale=4, bandlimit_type=bl, device=dev)
+    planes = prop.propagate_planes(field, zs).cpu().numpy()
+    assert planes.shape == (len(zs), 2, 1, 100, 100)
+    for k, z in enumerate(zs):
+        ref = orc.asm_forward(torch.from_numpy(x).to(torch.complex128), wavelengths([300], True),
+                              spacing(1.0, 1.0, True), z, 4, bandlimit_type=bl).numpy()
+        ref32 = orc.asm_forward(torch.from_numpy(x), wavelengths([300]), spacing(1.0, 1.0), z, 4,
+                                bandlimit_type=bl).numpy()
+        floor = rel_l2(ref32, ref)
+        assert rel_l2(planes[k], ref) <= max(1e-4, 1.5 * floor), (k, z, floor)
+    from quantizationawarethzdoe_amd.propagation import asm_apply
+    gen = torch.Generator(device=dev).manual_seed(9)
+    r = torch.randn(2, 1, 100, 100, dtype=torch.complex64, device=dev, generator=gen)
+    y = torch.randn(len(zs), 2, 1, 100, 100, dtype=torch.complex64, device=dev, generator=gen)
+    code = 1 if bl == "exact" else 2
+    Ax = asm_apply(r, [wl], [1e-3, 1e-3], zs, 200, 200, True, code)
+    AHy = asm_apply(y, [wl], [1e-3, 1e-3], zs, 200, 200, True, code, adjoint=True)
+    lhs = torch.vdot(y.reshape(-1).to(torch.complex128), Ax.reshape(-1).to(torch.complex128))
+    rhs = torch.vdot(AHy.reshape(-1).to(torch.complex128), r.reshape(-1).to(torch.complex128))
+    assert abs(complex(lhs - rhs)) / abs(complex(lhs)) <= 1e-4
+
+
 def test_asm_max_planes_per_call():
     """THZ_MAX_Z = 256 planes in one call (8 default z-chunks of 32, P = 1024): every 32nd plane
     and both chunk edges vs the fp64 oracle at <= max(1e-4, 1.5 x the fp32 oracle's error)."""
@@ -407,6 +442,8 @@ def test_asm_largest_transform_p16384_properties():
     (80, 72, 1.5, "approx", 2, 5, 0),       # runtime plan (P = 200 / 180), one chunk
     (100, 100, 2, "exact", 1, 4, 0),        # P = 300: the mixed-radix column pass
     (100, 100, 2, "exact", 1, 7, 3),        # P = 300, three chunks (the later ones add into U)
+    (100, 100, 4, "exact", 1, 5, 0),        # P = 500: the compile-time 5 4 5 5 plan (extended DOF)
+    (100, 100, 4, "exact", 2, 5, 2),        # P = 500, two wavelengths, three chunks
     (512, 512, 1, "exact", 2, 5, 2),        # P = 1024: the power-of-two column pass, three chunks
     (1024, 1024, 1, "exact", 1, 3, 0),      # P = 2048
     (60, 70, 1, "none", 1, 3, 0),           # no band limit

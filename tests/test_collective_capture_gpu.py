@@ -88,6 +88,44 @@ def test_donn_captured_allreduce_matches_split_graphs(one_rank_rccl):
           f"captured {res[True][2]:.4f} ms")
 
 
+@pytest.mark.parametrize("trainer", ["qat", "donn"])
+def test_capture_collective_refused_without_the_event_cache_setting(one_rank_rccl, monkeypatch, trainer):
+    """with TORCH_NCCL_CUDA_EVENT_CACHE not 0 in the process
+    (qat.collective_capture_safe) a trainer asked to capture the all-reduce keeps it out of the
+    graph: split graphs around the eager collective, a RuntimeWarning naming the variable, and the
+    same trajectory as the split form asked for directly."""
+    import warnings
+    from quantizationawarethzdoe_amd import donn, qat
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(3)
+    u = torch.rand(8, 1, 100, 100, generator=g).to(dev)
+    labels = torch.randint(0, 10, (8,), generator=g).to(dev)
+    res = {}
+    for capture in (False, True):
+        torch.manual_seed(5)
+        if trainer == "qat":
+            system = qat.FourFocalSpotsSystem(device=dev)
+            tr = qat.QATTrainer(system, qat.four_focal_spots_target(device=dev), graph=True, force_collective=True,
+                                capture_collective=capture)
+            step = lambda f: tr.step(f)  # noqa: E731
+        else:
+            model = donn.DONN(device=dev)
+            tr = donn.DONNTrainer(model, donn.detector_targets(device=dev), graph=True, force_collective=True,
+                                  capture_collective=capture)
+            step = lambda f: tr.step(u, labels, f)  # noqa: E731
+        with monkeypatch.context() as mp_:
+            mp_.setenv("TORCH_NCCL_CUDA_EVENT_CACHE", "1")
+            with warnings.catch_warnings(record=True) as rec:
+                warnings.simplefilter("always")
+                losses = [float(step(f)) for f in (0.1, 0.5, 0.9)]
+        assert not tr.capture_collective
+        assert all(g_opt is not None for _, g_opt, _ in tr._graphs.values())  # split form everywhere
+        if capture:
+            assert any("TORCH_NCCL_CUDA_EVENT_CACHE" in str(w.message) for w in rec)
+        res[capture] = losses
+    assert res[True] == res[False]
+
+
 @pytest.mark.parametrize("which", ["qat", "donn", "qat_full", "donn_eager_first"])
 def test_captured_trainers_keep_no_autograd_graph_alive(which):
     """the captured trainers used to keep a step's autograd graph alive (the DOE

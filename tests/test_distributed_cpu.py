@@ -132,6 +132,56 @@ def _agree_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _guard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # rank 0's environment makes the capture safe, rank 1's does not (the variable unset)
+    if rank == 0:
+        os.environ["TORCH_NCCL_CUDA_EVENT_CACHE"] = "0"
+    else:
+        os.environ.pop("TORCH_NCCL_CUDA_EVENT_CACHE", None)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import warnings
+        from quantizationawarethzdoe_amd.qat import GradientAllReduce, agreed_capture, collective_capture_safe
+        ar = GradientAllReduce([torch.nn.Parameter(torch.zeros(4))])
+        ar.capturable = True  # as on RCCL: the collective would be captured into the graph
+        called = []
+
+        def capture():
+            called.append(rank)
+            return "graph", 1.0
+
+        with warnings.catch_warnings(record=True) as rec:
+            warnings.simplefilter("always")
+            res = agreed_capture(ar, capture)
+        warned = any("TORCH_NCCL_CUDA_EVENT_CACHE" in str(w.message) for w in rec)
+        q.put((rank, collective_capture_safe(), res, bool(called), warned))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_capture_guard_falls_back_on_every_rank_gloo_world2():
+    """the library itself refuses to capture the all-reduce where
+    TORCH_NCCL_CUDA_EVENT_CACHE is not 0 (qat.collective_capture_safe).  The rank without the
+    variable does not attempt the capture and votes for the split form, so BOTH ranks fall back
+    (agreed_capture's MIN), with the variable named in the warning."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_guard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, safe0, res0, called0, _), (r1, safe1, res1, called1, warned1) = res
+    assert safe0 and not safe1
+    assert res0 is None and res1 is None          # every rank takes the split form
+    assert called0 and not called1                # rank 1 never attempted the capture
+    assert warned1
+
+
 def test_agreed_capture_falls_back_on_every_rank_gloo_world2():
     """a capture failure on ONE rank makes every rank take the split form (the
     eager MIN of a success flag after the attempt); a capture that succeeds everywhere is kept."""

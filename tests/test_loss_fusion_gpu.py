@@ -174,7 +174,9 @@ def test_loss_near_convergence_vs_fp64_oracle(fused):
     (delta ~ 6e-8), which shifts every residual coherently by -(I/m) delta; the argmax element's
     term S / m^2 (S = sum_i r_i I_i, a random-sign sum of n = 10^4 residuals of ~1e-4) moves by
     ~delta sqrt(n) / 1e-4 ~ 6 %, and that element carries ~40 % of the gradient's norm here
-    (measured on the box: 1.5e-2 rel-L2, all of it at the two argmax elements).  Bound 0.1."""
+    (measured on the box: 1.5e-2 rel-L2, all of it at the two argmax elements).  Bound 0.1 on the whole
+    gradient; with the two argmax elements masked the old bound, 1e-2, and at each argmax element
+    0.25 relative."""
     from quantizationawarethzdoe_amd import optics, propagation as P
     dev = _dev()
     g = torch.Generator().manual_seed(8)
@@ -222,6 +224,19 @@ def test_loss_near_convergence_vs_fp64_oracle(fused):
     assert 1e-10 < rv < 1e-6, rv  # near convergence: the loss is ~1e-8 of the target's scale
     assert abs(lv - rv) <= 1e-2 * rv, (lv, rv)
     assert rel_l2(gx.cpu().numpy(), rg.numpy()) <= (1e-2 if fused else 0.1)
+    if not fused:
+        # (b) at the old bound with the argmax elements masked: everywhere
+        # else the fp64 oracle's gradient is met to 1e-2; at the argmax element itself the coherent
+        # S / m^2 shift (~6 %, above) is bounded separately
+        Io = (Eo.detach().abs() ** 2).reshape(2, -1)
+        amo = Io.argmax(dim=1)
+        ga, gr = gx.cpu().reshape(2, -1).clone(), rg.reshape(2, -1).clone()
+        at_max = [(ga[b, amo[b]], gr[b, amo[b]]) for b in range(2)]
+        ga[torch.arange(2), amo] = 0
+        gr[torch.arange(2), amo] = 0
+        assert rel_l2(ga.numpy(), gr.numpy()) <= 1e-2, rel_l2(ga.numpy(), gr.numpy())
+        for a, b_ in at_max:
+            assert abs(complex(a) - complex(b_)) <= 0.25 * abs(complex(b_)), (complex(a), complex(b_))
 
 
 @pytest.mark.parametrize("how", ["wavelength_f64", "data_c128"])
