@@ -1,5 +1,5 @@
 """The plane recurrence of the power-of-two column pass (csrc/thz_asm.hip asm_cols_body,
-plane_recurrence_ok): for a uniform z-sweep (cfg2's linspace, experiment_extend_depth_of_focus.ipynb:229)
+recurrence_step_ok): for a uniform z-sweep (cfg2's linspace, experiment_extend_depth_of_focus.ipynb:229)
 the column pass advances G_j = sp H_{z_j} by one complex product per plane instead of one sincos
 per element per plane (Props/ASM_Prop.py:257-262 evaluates exp(i z sqrt(k^2 - K^2)) per plane).
 
@@ -95,12 +95,13 @@ def test_recurrence_split_chunks_and_kparts():
     [0.04, 0.07],                             # two planes
 ], ids=["nonuniform", "eps_too_large", "two_planes"])
 def test_non_uniform_planes_keep_the_sincos_path(zs):
-    """plane_recurrence_ok refuses these lists: both settings of the switch run the same kernel
+    """recurrence_step_ok refuses these lists: both settings of the switch run the same kernel
     code path and give bit-identical planes."""
     x, lam, sp = _narrow_input(512, 5)
     a = _run(x, lam, sp, zs, 256, True)
     b = _run(x, lam, sp, zs, 256, False)
     assert torch.equal(a, b)
+    assert b.abs().amax() > 0
 
 
 def test_wide_band_columns_keep_the_sincos_path():
@@ -115,6 +116,7 @@ def test_wide_band_columns_keep_the_sincos_path():
     a = _run(x, lam, sp, zs, 256, True)
     b = _run(x, lam, sp, zs, 256, False)
     assert torch.equal(a, b)
+    assert b.abs().amax() > 0
 
 
 def test_recurrence_two_wavelengths_and_batch():

@@ -11,7 +11,16 @@ is on robust statistics: the median over seeds of the mean of the last 100 itera
 minimum, and the loss at iterations 200 / 400 within [0.5x, 2x] of the span of the two reference
 runs (the saved curve and the printed trace differ by up to 1.5x there).  scripts/qat_quality.py
 runs every method of the notebook with five seeds (profiles/r04_qat_quality.json), and with
---system dual / edof the methods of the dual-plane and extended-DOF notebooks (profiles/r05_*)."""
+--system dual / edof the methods of the dual-plane and extended-DOF notebooks (profiles/r05_*).
+
+The published curves are ONE unseeded CUDA run each.  tests/golden/qat_ref_runs.json holds the
+REFERENCE ITSELF run here on CPU for the four-focal-spots and extended-DOF methods, three seeds
+each, 6,000 iterations (tests/golden/gen_qat_ref_runs.py): where it has a method, the HIP runs are
+graded against that same-code spread -- the median over the HIP seeds of the final loss, the minimum
+and the mean of the last 100 iterations each within [min / 1.25, max x 1.25] over the reference's
+seeds -- and the published curve is reported but not the bound (the reference's own seeds span up
+to 3.6x at the final loss, and the published extended-DOF runs sit at the low end of them).  The
+dual-plane methods (no reference runs) keep the published-curve band [0.5x, 2x]."""
 import json
 import os
 
@@ -22,6 +31,29 @@ import torch
 from tests.golden_io import GOLDEN
 
 pytestmark = pytest.mark.gpu
+SAME_CODE_SLACK = 1.25
+
+
+def ref_runs(system, method):
+    """The reference's own seeded runs of (system, method), or None (tests/golden/qat_ref_runs.json)."""
+    path = os.path.join(GOLDEN, "qat_ref_runs.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        runs = json.load(fh)["runs"].get(f"{system}/{method}")
+    return runs if runs and len(runs) >= 3 else None
+
+
+def assert_within_reference_runs(system, method, hip_stats):
+    """The HIP seeds' median of each statistic within [min / 1.25, max x 1.25] of the reference's
+    own seeds (same code, same iterations)."""
+    runs = ref_runs(system, method)
+    assert runs is not None, (system, method)
+    for k in ("final", "min", "mean_last100"):
+        med = float(np.median([s[k] for s in hip_stats]))
+        lo = min(r[k] for r in runs) / SAME_CODE_SLACK
+        hi = max(r[k] for r in runs) * SAME_CODE_SLACK
+        assert lo <= med <= hi, (system, method, k, med, lo, hi)
 
 
 def test_v3_six_thousand_iterations_within_the_reference_envelope():
@@ -43,6 +75,7 @@ def test_v3_six_thousand_iterations_within_the_reference_envelope():
     mn = float(np.median([s["min"] for s, _ in runs]))
     assert 0.5 * r["mean_last100"] <= last100 <= 2.0 * r["mean_last100"], (last100, r["mean_last100"])
     assert 0.5 * r["min"] <= mn <= 2.0 * r["min"], (mn, r["min"])
+    assert_within_reference_runs("four_focal", "Ours", [s for s, _ in runs])
     for it in (200, 400):
         lo = min(r["trace"][it // 200], printed[it])
         hi = max(r["trace"][it // 200], printed[it])
@@ -72,17 +105,15 @@ def test_naive_gumbel_six_thousand_iterations_stay_finite_and_within_the_envelop
     mn = float(np.median([s["min"] for s in runs]))
     assert 0.5 * r["mean_last100"] <= last100 <= 2.0 * r["mean_last100"], (last100, r["mean_last100"])
     assert 0.5 * r["min"] <= mn <= 2.0 * r["min"], (mn, r["min"])
+    assert_within_reference_runs("four_focal", "GS", runs)
 
 
 ENVELOPE_CASES = [
-    # (system, method): example_1's remaining methods and every method of
-    # the two multi-plane systems (item 2) -- except the extended-DOF STE run, whose median minimum
-    # is 2.6x the reference's (its last-100 mean 1.9x; profiles/r05_qat_quality_edof.json: the
-    # extended-DOF runs sit at 1.1-1.5x of the reference's curves for every other method, the
-    # dual-plane ones at 0.9-1.05x)
+    # every remaining method of the three notebooks (four-focal "Ours" and GS: the tests above),
+    # graded against the reference's own seeded runs where tests/golden/qat_ref_runs.json has them
     ("four_focal", "STE"), ("four_focal", "PSQ"), ("four_focal", "full"),
     ("dual", "Ours"), ("dual", "full"), ("dual", "GQ"), ("dual", "PSQ"), ("dual", "STE"),
-    ("edof", "Ours"), ("edof", "full"), ("edof", "GQ"), ("edof", "PSQ"),
+    ("edof", "Ours"), ("edof", "full"), ("edof", "STE"), ("edof", "GQ"), ("edof", "PSQ"),
 ]
 
 
@@ -90,9 +121,10 @@ ENVELOPE_CASES = [
 def test_six_thousand_iterations_within_the_reference_envelope(system, method):
     """The notebook's whole 6,000-iteration run of one method of one system (scripts/qat_quality.py:
     the layer, optim_params, optimiser and lr of its cell), three seeds on the graph-replayed
-    trainer: every loss finite, the median over seeds of the mean of the last 100 iterations and of
-    the minimum within [0.5x, 2x] of the reference's own curve (plot_data/example_1, _2 or _3
-    loss_curve_<method>.npy via tests/golden/qat_curves.json).  The multi-plane systems propagate
+    trainer: every loss finite; against the reference's own seeded runs where they exist (module
+    docstring), else the median over seeds of the mean of the last 100 iterations and of the minimum
+    within [0.5x, 2x] of the published curve (plot_data/example_1, _2 or _3 loss_curve_<method>.npy
+    via tests/golden/qat_curves.json).  The multi-plane systems propagate
     their planes in one pipeline with the Z-summing adjoint; the extended-DOF planes move every
     iteration (read from the device step state) and its P = 500 transforms run the runtime
     mixed-radix plan."""
@@ -109,5 +141,10 @@ def test_six_thousand_iterations_within_the_reference_envelope(system, method):
         runs.append(stats(curve))
     last100 = float(np.median([s["mean_last100"] for s in runs]))
     mn = float(np.median([s["min"] for s in runs]))
-    assert 0.5 * r["mean_last100"] <= last100 <= 2.0 * r["mean_last100"], (last100, r["mean_last100"])
-    assert 0.5 * r["min"] <= mn <= 2.0 * r["min"], (mn, r["min"])
+    print(f"\n{system}/{method}: HIP median last100 {last100:.3e} min {mn:.3e}; published "
+          f"{r['mean_last100']:.3e} / {r['min']:.3e} ({last100 / r['mean_last100']:.2f}x / {mn / r['min']:.2f}x)")
+    if ref_runs(system, method) is not None:
+        assert_within_reference_runs(system, method, runs)
+    else:
+        assert 0.5 * r["mean_last100"] <= last100 <= 2.0 * r["mean_last100"], (last100, r["mean_last100"])
+        assert 0.5 * r["min"] <= mn <= 2.0 * r["min"], (mn, r["min"])
