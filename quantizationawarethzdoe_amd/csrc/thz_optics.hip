@@ -148,13 +148,21 @@ __global__ void __launch_bounds__(FIN_THREADS) loss_finish_kernel(LossSink ls) {
     ls.stats[3 * b + 0] = m;
     ls.stats[3 * b + 1] = __int_as_float((int)(0xffffffffu - (unsigned)acc.key));
     ls.stats[3 * b + 2] = (float)(acc.ii / md - acc.it);
-    // the term written through to memory (an agent-scope atomic store) and its completion awaited
-    // before the arrival is counted: the release the last workgroup needs, without the L2
-    // write-back of an agent-scope fence (which every one of B workgroups would pay)
-    __hip_atomic_store(ls.terms() + b, acc.ii / (md * md) - 2.0 * acc.it / md + acc.tt, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
-    s_last = atomicAdd(ls.counter(), 1ull) == (unsigned long long)(ls.B - 1);
+    if (ls.B == 1) {
+      // one item (cfg4): its term is the sum -- the same value the path below forms (0.0 + x and
+      // x + 0.0 are exact), without its write-through store, arrival atomic and reload: three
+      // dependent memory round trips of a kernel every QAT step runs
+      ls.loss[0] = (float)((acc.ii / (md * md) - 2.0 * acc.it / md + acc.tt) * ls.inv_n);
+      s_last = 0;
+    } else {
+      // the term written through to memory (an agent-scope atomic store) and its completion awaited
+      // before the arrival is counted: the release the last workgroup needs, without the L2
+      // write-back of an agent-scope fence (which every one of B workgroups would pay)
+      __hip_atomic_store(ls.terms() + b, acc.ii / (md * md) - 2.0 * acc.it / md + acc.tt, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0)
+      s_last = atomicAdd(ls.counter(), 1ull) == (unsigned long long)(ls.B - 1);
+    }
   }
   __syncthreads();
   if (!s_last) return;
@@ -325,30 +333,43 @@ struct AdamArgs {
   unsigned* done;
 };
 
-// the element update (torch's single-tensor Adam expressions, fp32)
-__device__ __forceinline__ void adam_elem(const AdamArgs& a, int q, long long i, float nstep, float bc2s) {
-  float p = a.p[q][i], g = a.g[q][i];
+// the element update (torch's single-tensor Adam expressions, fp32) on loaded values; returns p
+struct AdamElem {
+  float p, g, m, v;
+};
+__device__ __forceinline__ void adam_update(const AdamArgs& a, AdamElem& e, float nstep, float bc2s) {
+  float p = e.p, g = e.g;
   if (a.decoupled) p = p * a.decay;
   else if (a.wd != 0.0f) g = g + a.wd * p;
-  const float m0 = a.m[q][i];  // lerp(m0, g, w) as ATen evaluates it
+  const float m0 = e.m;  // lerp(m0, g, w) as ATen evaluates it
   const float w = a.omb1;
-  const float m = w < 0.5f ? m0 + w * (g - m0) : g - (g - m0) * (1.0f - w);
-  const float v = a.v[q][i] * a.b2f + (a.omb2 * g) * g;
-  a.m[q][i] = m;
-  a.v[q][i] = v;
-  a.p[q][i] = p + nstep * (m / (sqrtf(v) / bc2s + a.eps));
+  e.m = w < 0.5f ? m0 + w * (g - m0) : g - (g - m0) * (1.0f - w);
+  e.v = e.v * a.b2f + (a.omb2 * g) * g;
+  e.p = p + nstep * (e.m / (sqrtf(e.v) / bc2s + a.eps));
 }
 
 // A workgroup is PER x 256 elements of one parameter: one per thread for the QAT maps (a
 // one-workgroup loop over a 2,500-element map ran 2-3x longer, its loads in sequence), four for
 // larger sets (the DONN's 30,000: 30 workgroups instead of 118, each with its release fence).  Thread q < np reads parameter q's step
 // count and forms its scalars (fp64 bias corrections); the last workgroup to finish advances the
-// counts, after every workgroup has read them.
+// counts, after every workgroup has read them.  The elements' loads are issued first, so their
+// latency overlaps the step-count read and the fp64 pow of the bias corrections (before: after
+// the scalars' barrier, a third dependent memory round trip on the step's critical path).
 template <int PER>
 __global__ void __launch_bounds__(ADAM_THREADS) adam_step_kernel(AdamArgs a) {
   __shared__ float s_ns[THZ_MAX_ADAM_PARAMS], s_bs[THZ_MAX_ADAM_PARAMS];
   __shared__ int s_last;
   const int tid = threadIdx.x;
+  const int bid = blockIdx.x;
+  int q = 0;
+  while (q + 1 < a.np && bid >= a.blk0[q + 1]) ++q;
+  const long long i0 = (long long)(bid - a.blk0[q]) * (PER * ADAM_THREADS) + tid;
+  AdamElem e[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const long long i = i0 + (long long)k * ADAM_THREADS;
+    if (i < a.n[q]) e[k] = AdamElem{a.p[q][i], a.g[q][i], a.m[q][i], a.v[q][i]};
+  }
   float t = 0.0f;
   if (tid < a.np) {
     t = a.step[tid][0] + 1.0f;
@@ -357,14 +378,15 @@ __global__ void __launch_bounds__(ADAM_THREADS) adam_step_kernel(AdamArgs a) {
     s_bs[tid] = (float)sqrt(bc2);
   }
   __syncthreads();
-  const int bid = blockIdx.x;
-  int q = 0;
-  while (q + 1 < a.np && bid >= a.blk0[q + 1]) ++q;
-  const long long i0 = (long long)(bid - a.blk0[q]) * (PER * ADAM_THREADS) + tid;
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     const long long i = i0 + (long long)k * ADAM_THREADS;
-    if (i < a.n[q]) adam_elem(a, q, i, s_ns[q], s_bs[q]);
+    if (i < a.n[q]) {
+      adam_update(a, e[k], s_ns[q], s_bs[q]);
+      a.m[q][i] = e[k].m;
+      a.v[q][i] = e[k].v;
+      a.p[q][i] = e[k].p;
+    }
   }
   // no release fence: nothing this workgroup wrote is read by the last one, and its step-count read
   // (thread q, above) has returned before the arrival is counted (the count's value is already used)
