@@ -13,6 +13,7 @@ a barrier + synchronize bracket the timed region and the max time over ranks cou
     python bench.py [--gpus N] [--steps K] [--warmup W]
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -739,8 +740,8 @@ def _secondary_watchdog(line, keys, rank, timeout_s, snapshot):
                 done.setdefault(k, {"error": f"timed out after {timeout_s:.0f} s (watchdog)"})
             if rank == 0:
                 out = dict(line, secondary=done)
-                sys.stdout.write(json.dumps(out) + "\n")
-                sys.stdout.flush()
+                sys.__stdout__.write(json.dumps(out) + "\n")
+                sys.__stdout__.flush()
             failed = _failed_checks(done)
             sys.stderr.write(f"bench.py: secondary measurements exceeded {timeout_s:.0f} s; exiting "
                              f"with status {WATCHDOG_EXIT}\n")
@@ -919,21 +920,24 @@ def main():
                 ("cfg4_extended_dof", lambda *a, **k: bench_qat_multi(*a, which="edof", **k)),
                 ("cfg5_donn", bench_donn))
         watchdog = _secondary_watchdog(line, [k for k, _ in secs], rank, args.secondary_timeout, snapshot)
-        for key, fn in secs:
-            try:
-                res = fn(dev, rank, world, dist=ranks.dist)
-            except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-                res = {"error": f"{type(e).__name__}: {e}"[:300]}
-            secondary[key] = res
-            snapshot[0] = dict(secondary)  # one reference swap: the watchdog reads a finished copy
-        if world == 1 and not args.no_shares:
-            try:
-                res = per_rank_shares(dev, x, lam, sp)
-            except Exception as e:  # noqa: BLE001 -- reported in the JSON line
-                res = {"error": f"{type(e).__name__}: {e}"[:300]}
-            secondary["per_rank_share_n8"] = res
-            snapshot[0] = dict(secondary)
-        watchdog.cancel()
+        # the propagators' own diagnostics (the reference's critical-distance print) go to stderr:
+        # stdout carries the one JSON line
+        with contextlib.redirect_stdout(sys.stderr):
+            for key, fn in secs:
+                try:
+                    res = fn(dev, rank, world, dist=ranks.dist)
+                except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+                    res = {"error": f"{type(e).__name__}: {e}"[:300]}
+                secondary[key] = res
+                snapshot[0] = dict(secondary)  # one reference swap: the watchdog reads a finished copy
+            if world == 1 and not args.no_shares:
+                try:
+                    res = per_rank_shares(dev, x, lam, sp)
+                except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+                    res = {"error": f"{type(e).__name__}: {e}"[:300]}
+                secondary["per_rank_share_n8"] = res
+                snapshot[0] = dict(secondary)
+            watchdog.cancel()
         line["secondary"] = secondary
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.cpu_budget, args.cpu_planes)
