@@ -12,6 +12,12 @@ Systems, exactly as the notebook cells (see gen_qat_multi.py / gen_golden.gen_qa
     (doe_params of cell 1, optim_params c_s 100, tau 2.5 -> 1.5 except PSQ's c_s 300, tau 400 -> 1)
     -> five ASM planes at 50..90 mm re-drawn after every forward; loss = sum of the five
     MSE(normalize(|E|^2), PSF(f = 100 mm)); lr 0.02, AdamW ("Ours", STE, "full") or Adam (GQ, PSQ).
+  * dual (plot_data/example_2/experiment_dual_plane_hologram.ipynb cells 2-8 "Ours", 16-18 "full",
+    39-41 GQ, 46-48 PSQ, 53-55 STE): the same optics with padding 2, the second 127 mm propagation
+    before the aperture in every cell but "Ours" (cell 6 comments it out), tolerance 50 um, tan d
+    0.003, num_unit None, planes at 100 and 150 mm against the two Aalto logos (the package's decoded
+    copy, data/dual_plane_targets.npz, made by gen_qat_multi.py from the notebook's cells 3-4); loss =
+    the two MSEs summed; lr 0.01, AdamW ("Ours", "full", GQ) or Adam (PSQ, STE; c_s 300, tau 800 -> 1).
   * four_focal (experiment_four_focal_spots.ipynb "Ours" 6-8, "full" 19-22, GS 31-33, PSQ 41-43,
     STE 50-52): the 9-spot target at 200 mm, padding 2, num_unit 2; GS c_s 100, tau 5.5 -> 1.0;
     PSQ and STE c_s 300, tau 400 -> 1 (cell 42's dict, still in force at cell 51); lr 0.02, Adam
@@ -112,6 +118,15 @@ EDOF = {
 }
 
 
+DUAL = {
+    "Ours": ("SoftGumbelQuantizedDOELayerv3", None, "adamw", False),
+    "full": ("FullPrecisionDOELayer", None, "adamw", True),
+    "GQ": ("NaiveGumbelQuantizedDOELayer", None, "adamw", True),
+    "PSQ": ("PSQuantizedDOELayer", dict(c_s=300, tau_max=800, tau_min=1), "adam", True),
+    "STE": ("STEQuantizedDOELayer", dict(c_s=300, tau_max=800, tau_min=1), "adam", True),
+}
+
+
 def optics_before_doe2(ref, pad, second):
     """optics_before_doe with the optional second ASM 127 mm after the lens (cells whose
     field_before_DOE runs asm_prop2)."""
@@ -157,6 +172,20 @@ def run(system, method, seed, iters):
                                   device="cpu") for z in (50, 60, 70, 80, 90)]
         jitter = [(50, 0, 5), (60, -5, 5), (70, -5, 5), (80, -5, 5), (90, -5, 0)]
         targets = [target] * 5
+    elif system == "dual":
+        doe_params = dict(doe_size=[100, 100], doe_dxy=1 * MM, doe_level=4, look_up_table=None, num_unit=None,
+                          height_constraint_max=1 * MM, tolerance=0.05 * MM, material=[2.66, 0.003])
+        cls, op, optname, second = DUAL[method]
+        optim_params = op or dict(c_s=100, tau_max=2.5, tau_min=1.5)
+        tt = np.load(os.path.join(os.path.dirname(os.path.dirname(HERE)), "quantizationawarethzdoe_amd", "data",
+                                  "dual_plane_targets.npz"))["targets"].astype(np.float32)
+        field_in = optics_before_doe2(ref, 2, second)
+        torch.manual_seed(seed)
+        doe = make_layer(ref, cls, doe_params, optim_params)
+        props = [ref.ASM.ASM_prop(z_distance=z * MM, bandlimit_type='exact', padding_scale=2, bandlimit_kernel=True,
+                                  device="cpu") for z in (100, 150)]
+        jitter = None
+        targets = [torch.from_numpy(tt[i]).reshape(1, 1, 100, 100) for i in range(2)]
     elif system == "four_focal":
         doe_params = dict(doe_size=[100, 100], doe_dxy=1 * MM, doe_level=4, look_up_table=None, num_unit=2,
                           height_constraint_max=1 * MM, tolerance=10e-6, material=[2.66, 0.03])
@@ -173,7 +202,8 @@ def run(system, method, seed, iters):
         targets = [target]
     else:
         raise SystemExit(f"unknown system {system}")
-    opt = (torch.optim.AdamW if optname == "adamw" else torch.optim.Adam)(doe.parameters(), lr=0.02)
+    lr = 0.01 if system == "dual" else 0.02
+    opt = (torch.optim.AdamW if optname == "adamw" else torch.optim.Adam)(doe.parameters(), lr=lr)
     torch.manual_seed(seed)
     random.seed(seed)
     losses = []
@@ -217,7 +247,7 @@ def merge(key, entry):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--system", required=True, choices=["edof", "four_focal"])
+    ap.add_argument("--system", required=True, choices=["edof", "four_focal", "dual"])
     ap.add_argument("--method", required=True)
     ap.add_argument("--seed", type=int, required=True)
     ap.add_argument("--iters", type=int, default=6000)

@@ -14,13 +14,12 @@ runs every method of the notebook with five seeds (profiles/r04_qat_quality.json
 --system dual / edof the methods of the dual-plane and extended-DOF notebooks (profiles/r05_*).
 
 The published curves are ONE unseeded CUDA run each.  tests/golden/qat_ref_runs.json holds the
-REFERENCE ITSELF run here on CPU for the four-focal-spots and extended-DOF methods, three seeds
-each, 6,000 iterations (tests/golden/gen_qat_ref_runs.py): where it has a method, the HIP runs are
-graded against that same-code spread -- the median over the HIP seeds of the minimum and of the
-mean of the last 100 iterations each within [min / 1.25, max x 1.25] over the reference's seeds and
-its published run (the reference's own seeds span up to 3.6x at the final loss, and the
-published extended-DOF runs sit at the low end of them).  The
-dual-plane methods (no reference runs) keep the published-curve band [0.5x, 2x]."""
+REFERENCE ITSELF run here on CPU for every method of the three notebooks, three seeds each, 6,000
+iterations (tests/golden/gen_qat_ref_runs.py): the HIP runs are graded against that same-code
+spread -- the median over the HIP seeds of the minimum and of the mean of the last 100 iterations
+each within [min / 1.25, max x 1.25] over the reference's seeds and its published run (the
+reference's own seeds span up to 3.6x at the final loss, and the published extended-DOF runs sit at
+the low end of them)."""
 import json
 import os
 
@@ -133,8 +132,8 @@ def test_six_thousand_iterations_within_the_reference_envelope(system, method):
     within [0.5x, 2x] of the published curve (plot_data/example_1, _2 or _3 loss_curve_<method>.npy
     via tests/golden/qat_curves.json).  The multi-plane systems propagate
     their planes in one pipeline with the Z-summing adjoint; the extended-DOF planes move every
-    iteration (read from the device step state) and its P = 500 transforms run the runtime
-    mixed-radix plan."""
+    iteration (read from the device step state) and its P = 500 transforms run the compile-time
+    5 4 5 5 plan."""
     import sys
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts"))
     from qat_quality import reference, run_method, stats

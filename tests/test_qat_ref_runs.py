@@ -24,6 +24,7 @@ def test_reference_runs_complete_and_finite():
     d = _load()
     keys = {f"{s}/{m}" for s in ("four_focal",) for m in ("Ours", "full", "GS", "PSQ", "STE")}
     keys |= {f"edof/{m}" for m in ("Ours", "full", "STE", "GQ", "PSQ")}
+    keys |= {f"dual/{m}" for m in ("Ours", "full", "GQ", "PSQ", "STE")}
     assert keys <= set(d["runs"]), sorted(keys - set(d["runs"]))
     for key, runs in d["runs"].items():
         assert sorted(r["seed"] for r in runs) == [0, 1, 2], key
@@ -35,7 +36,7 @@ def test_reference_runs_complete_and_finite():
             assert r["min"] <= r["final"] and r["min"] <= r["mean_last100"]
 
 
-@pytest.mark.parametrize("system", ["four_focal", "edof"])
+@pytest.mark.parametrize("system", ["four_focal", "edof", "dual"])
 def test_generator_runs_the_hip_runners_cells(system):
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
@@ -47,8 +48,8 @@ def test_generator_runs_the_hip_runners_cells(system):
     ns = {}
     start = src.index("FOUR_FOCAL = {")
     end = src.index("def optics_before_doe2")
-    exec(compile(src[start:end], spec.origin, "exec"), ns)  # two literal dicts
-    gen = ns["FOUR_FOCAL" if system == "four_focal" else "EDOF"]
+    exec(compile(src[start:end], spec.origin, "exec"), ns)  # three literal dicts
+    gen = ns[{"four_focal": "FOUR_FOCAL", "edof": "EDOF", "dual": "DUAL"}[system]]
     hip = SYSTEMS[system]["methods"]
     assert set(gen) == set(hip)
     default = {"c_s": 100, "tau_max": 2.5, "tau_min": 1.5}
