@@ -363,7 +363,12 @@ __global__ void __launch_bounds__(64 * CZB_W) __attribute__((amdgpu_waves_per_eu
 constexpr int CZB_WC = CB / 2;  // columns pass: 8 columns (waves) per workgroup
 constexpr int CZB_IMS = wf::IMG + 4;  // wave image stride: +4 floats skews the images' banks for the block writes
 constexpr int CZB_IMM = 544;          // imaginary parts of the staged column, float offset in the image
-constexpr size_t czb_cols_lds_bytes() { return wf::TAB * sizeof(float2) + CZB_WC * CZB_IMS * sizeof(float); }
+// + the block's filter spectrum G_b, shared by the workgroup's 8 columns (one wavelength), staged
+// in LDS with the block: its MACs read LDS instead of issuing 16 dependent L2 loads per lane
+// (czt_cols 0.176-0.180 -> 0.166-0.168 ms at cfg3, profiles/r06_experiments.txt 8)
+constexpr size_t czb_cols_lds_bytes() {
+  return wf::TAB * sizeof(float2) + CZB_WC * CZB_IMS * sizeof(float) + wf::N * sizeof(float2);
+}
 
 template <bool PARTIAL>
 __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_eu(CZB_WPE))) czt_cols_blk(const float2* __restrict__ V, float2* __restrict__ out,
@@ -374,6 +379,7 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* const img0 = reinterpret_cast<float*>(lds + wf::TAB);
   float* img = img0 + wave * CZB_IMS;
+  float2* const gl = reinterpret_cast<float2*>(img0 + CZB_WC * CZB_IMS);  // G_b of the current block
   {
     int off = 0;
     asm volatile("" : "+v"(off));  // keep the image base in the address register (wf::wave_image)
@@ -406,6 +412,9 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
     const int h0 = CZB_BS * b;
     // the half block's [CZB_BS rows][8 columns]: 4 x 16 B per thread (row e / 4, columns 2 (e % 4) + {0, 1})
     float4 t4[4];
+    static_assert(2 * 64 * CZB_WC == wf::N, "two spectrum values per thread");
+    const float2* Gs = G + (size_t)b * wf::N + 2 * threadIdx.x;
+    const float2 g0 = Gs[0], g1 = Gs[1];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = (int)threadIdx.x + 64 * CZB_WC * i;
@@ -428,11 +437,13 @@ __global__ void __launch_bounds__(64 * CZB_WC) __attribute__((amdgpu_waves_per_e
       d1[0] = t4[i].z;
       d1[CZB_IMM] = t4[i].w;
     }
+    gl[2 * threadIdx.x] = g0;
+    gl[2 * threadIdx.x + 1] = g1;
     __syncthreads();
     if (live) {
       int ln = lane;
       asm volatile("" : "+v"(ln));
-      const float2* Gb = G + (size_t)b * wf::N + ln;
+      const float2* Gb = gl + ln;
       auto mac = [&](int i, float2 x) { acc[i] = cadd(acc[i], cmul(x, Gb[64 * (i >> 2) + 256 * (i & 3)])); };
       auto ldb = [&](int u) {
         if (PARTIAL && h0 + u >= m) return make_float2(0.f, 0.f);
