@@ -33,7 +33,15 @@ __device__ __forceinline__ int xcd_chunk(int b, int nb) {
 // 8, 1.39 at 4, 1.33 unblocked, while the row pass gathers K3 1.05 ms at 16, 1.22 at 4, 2.59
 // unblocked; cfg2 sum per z-chunk lowest at 4), laid out as below.
 constexpr int CB = 16;
-constexpr int CBU = 4;
+#ifndef THZ_U_CBU
+#define THZ_U_CBU 4
+#endif
+#ifndef THZ_U_URT
+#define THZ_U_URT 4
+#endif
+constexpr int CBU = THZ_U_CBU;  // columns per U tile
+constexpr int URT = THZ_U_URT;  // rows per U tile (CBU x URT x 8 B = one 128-B line)
+static_assert(CBU * URT == 16, "a U tile is one 128-B line");
 __device__ __forceinline__ size_t blk(int c, int row, int rows) {
   return ((size_t)(c / CB) * rows + row) * CB + (c % CB);
 }
@@ -43,13 +51,15 @@ __device__ __forceinline__ size_t blk(int c, int row, int rows) {
 // 8 B of each of 4 sectors of a 128-B line.  The row-major CBU-column blocking it replaced had its
 // 32-B sectors written by the 4 column workgroups of a block: 1.65x U in WRITE_SIZE and K2 4.39 ->
 // 4.17 ms at cfg2 on the same box (profiles/r05_experiments.txt).  U's rows are padded to a
-// multiple of 4 (u_rows).
-__host__ __device__ constexpr int u_rows(int rows) { return (rows + 3) & ~3; }
+// multiple of URT (u_rows).  Taller tiles give the column pass more of each line (2 x 8: K2 -8 %,
+// 1 x 16: whole lines, K2 -8..-10 %) and cost the row pass more (K3 +33 %, +134 %:
+// profiles/r06_experiments.txt 9), so 4 x 4 stays.
+__host__ __device__ constexpr int u_rows(int rows) { return (rows + URT - 1) / URT * URT; }
 __device__ __forceinline__ size_t blk_u(int c, int row, int rows) {
-  return ((size_t)(c / CBU) * u_rows(rows) + (row & ~3)) * CBU + (c % CBU) * 4 + (row & 3);
+  return ((size_t)(c / CBU) * u_rows(rows) + (row & ~(URT - 1))) * CBU + (c % CBU) * URT + (row & (URT - 1));
 }
 // offset of row r from row 0 of the same column of U
-__device__ __forceinline__ size_t u_roff(int r) { return (size_t)(r & ~3) * CBU + (r & 3); }
+__device__ __forceinline__ size_t u_roff(int r) { return (size_t)(r & ~(URT - 1)) * CBU + (r & (URT - 1)); }
 
 
 // sin/cos of a float angle (|ang| up to ~1e5 rad): 3-constant Cody-Waite reduction by pi/2
