@@ -64,7 +64,8 @@ __global__ void __launch_bounds__(EW_THREADS) thin_lens_kernel(const float2* __r
     const int i = p / a.W, j = p - i * a.W;
     const float xg = lin(a.gx0, a.gx1, a.H, i) * a.dx;
     const float yg = lin(a.gy0, a.gy1, a.W, j) * a.dy;
-    const float r2 = xg * xg + yg * yg;
+    // x^2 + y^2 rounded term by term as the reference's xg ** 2 + yg ** 2 (no fma contraction)
+    const float r2 = __fadd_rn(__fmul_rn(xg, xg), __fmul_rn(yg, yg));
     float sn, cs;
     sincos_rad(-coef * r2, &sn, &cs);
     return make_float2(cs, sn);
@@ -489,8 +490,10 @@ extern "C" int thz_thin_lens(const thz_lens_desc* d, const void* in, void* out, 
   a.gy1 = (float)((d->W - 1) / 2);
   a.dx = d->dx;
   a.dy = d->dy;
+  // pi / (lambda f) in the reference's fp32 order: torch forms python_scalar / tensor as
+  // reciprocal(tensor) * scalar (Components/Thin_Lens.py:70-77), so one rounding more than a division
   const float PI = 3.14159265358979323846f;
-  for (int c = 0; c < d->C; ++c) a.coef[c] = PI / (d->wavelengths[c] * d->focal_length);
+  for (int c = 0; c < d->C; ++c) a.coef[c] = (1.0f / (d->wavelengths[c] * d->focal_length)) * PI;
   hipStream_t s = (hipStream_t)stream;
   KernelTimer kt("thin_lens", s);
   const int n = d->H * d->W;

@@ -18,7 +18,7 @@ import os
 import numpy as np
 import pytest
 import torch
-from hypothesis import HealthCheck, given, settings
+from hypothesis import HealthCheck, assume, example, given, settings
 from hypothesis import strategies as st
 
 from oracle import thz_oracle as orc
@@ -114,6 +114,42 @@ def test_asm_multi_plane_adjoint_is_the_sum_of_plane_adjoints(case):
     once = asm_apply(g, lam, sp, zs, ph, pw, True, 1, adjoint=True)
     summed = sum(asm_apply(g[k:k + 1], lam, sp, [z], ph, pw, True, 1, adjoint=True) for k, z in enumerate(zs))
     assert float((once - summed).norm() / summed.norm()) <= 1e-5
+
+
+@SETTINGS
+@given(st.fixed_dictionaries({"H": st.sampled_from([512, 1024]), "W": st.integers(200, 1024),
+                              "Z": st.integers(3, 12), "dx": st.sampled_from([0.2, 0.25, 0.5, 1.0]),
+                              "z0": st.floats(0.005, 0.2), "dz": st.floats(-0.02, 0.02),
+                              "f": st.floats(250.0, 350.0), "seed": st.integers(0, 2 ** 31 - 1)}))
+# found by a wide random sweep (k z = 1.9e3 rad at the last plane)
+@example({"seed": 70, "H": 512, "W": 510, "Z": 11, "dx": 0.25, "z0": 0.125, "dz": 0.015625, "f": 334.0})
+def test_asm_uniform_sweep_matches_single_planes(case):
+    """A uniform z-sweep on a power-of-two column length (padding scale 1: P = 1024 / 2048), where
+    the column pass may advance the planes by the plane recurrence (csrc/thz_asm.hip
+    recurrence_step_ok; taken per column when every step is an exact fp32 difference and the band
+    stays under P/4), against each plane propagated on its own (one plane: the per-plane sincos):
+    fp32 rel-L2 <= max(2e-5, 2^-25 k |z|) per plane, the first plane bit-identical.  (2e-5 is
+    tests/test_asm_recurrence_gpu.py's bound at cfg2's phases; the per-plane sincos form rounds its
+    phase z sq <= k |z| to fp32 -- up to half an ulp per element, ~3.6e-5 rel-L2 at k z ~ 1.9e3
+    rad in a wide random sweep -- while the recurrence carries the phase step in double.)"""
+    from quantizationawarethzdoe_amd.propagation import asm_apply, asm_padding
+    rng = np.random.default_rng(case["seed"])
+    H, W, Z = case["H"], case["W"], case["Z"]
+    zs = [float(v) for v in torch.linspace(case["z0"], case["z0"] + (Z - 1) * case["dz"], Z, dtype=torch.float32)]
+    assume(min(abs(z) for z in zs) >= 1e-3)
+    ph, pw = asm_padding(H, W, (1, 1))
+    lam = [float(np.float32(C0 / (case["f"] * 1e9)))]
+    sp = [float(np.float32(case["dx"] * 1e-3))] * 2
+    x = _rand(rng, (1, 1, H, W), torch.complex64)
+    multi = asm_apply(x, lam, sp, zs, ph, pw, True, 1)
+    for k, z in enumerate(zs):
+        one = asm_apply(x, lam, sp, [z], ph, pw, True, 1)[0]
+        if k == 0:
+            assert torch.equal(multi[0], one)
+        else:
+            e = float((multi[k] - one).norm() / one.norm())
+            kz = 2 * np.pi / lam[0] * abs(z)
+            assert e <= max(2e-5, kz * 2.0 ** -25), (k, z, e)
 
 
 @SETTINGS
@@ -385,6 +421,10 @@ def test_doe_layer_vs_oracle(case):
                               "kind": st.sampled_from(["rect", "circ"]), "size": st.floats(2e-3, 0.12),
                               "Ho": st.integers(1, 96), "Wo": st.integers(1, 96),
                               "zoom": st.sampled_from([0.25, 0.5, 1.0, 1.7, 3.0]), "seed": st.integers(0, 2 ** 31 - 1)}))
+# found by a wide random sweep: the lens coefficient formed as a correctly rounded division gave
+# 8.1e-6 against the reference's 3.4e-6 (torch forms pi / (lambda f) as reciprocal x pi)
+@example({"H": 83, "W": 2, "B": 1, "C": 1, "dx": 0.0013, "dy": 0.0005, "f": 0.07876511813361319, "kind": "rect",
+          "size": 0.0625, "Ho": 1, "Wo": 1, "zoom": 0.25, "seed": 0})
 def test_optics_elements_vs_oracle(case):
     """Thin lens (Components/Thin_Lens.py:31-85), aperture masks (Components/Aperture.py:61-118) and
     the field resampler (Addons/Field_Resampler.py:56-118) over drawn shapes, spacings, focal
