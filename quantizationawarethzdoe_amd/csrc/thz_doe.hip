@@ -379,10 +379,16 @@ __global__ void __launch_bounds__(256) quant_fwd_lv(QArgs a, const float* __rest
 __device__ __forceinline__ void quant_bwd_px(const QArgs& a, const QDyn& q, const float* __restrict__ w,
                                              const float* __restrict__ ysave, int p, int n, float G,
                                              float* __restrict__ gw) {
+  // The softmax backward in torch's form and rounding order (_softmax_backward_data:
+  // y_l (dy_l - sum_k dy_k y_k), the straight-through's dy_l = G lut_l formed first).  At a
+  // saturated softmax the difference keeps only the digits beyond the ulp of dy_l, as the
+  // reference's own does; a centred form sum_k y_k (dy_l - dy_k), exact there, multiplies the
+  // saturated level's rounding-noise score derivative by its now nonzero weight and moved a drawn
+  // case 10 % from fp64 where the reference sits at 7.5e-6 (profiles/r06_experiments.txt 10).
   if (a.kind == THZ_Q_NGS) {
     // d logits_l = y_l (dy_l - sum_k y_k dy_k) / tau, dy_l = G lut_l
     float dot = 0.f;
-    THZ_FOR_LEVELS(l, a.L) dot += ysave[(size_t)p * a.L + l] * G * a.lut[l];
+    THZ_FOR_LEVELS(l, a.L) dot += (G * a.lut[l]) * ysave[(size_t)p * a.L + l];
     THZ_FOR_LEVELS(l, a.L) {
       const float yl = ysave[(size_t)p * a.L + l];
       gw[(size_t)p * a.L + l] = yl * (G * a.lut[l] - dot) / q.tau;
@@ -391,7 +397,7 @@ __device__ __forceinline__ void quant_bwd_px(const QArgs& a, const QDyn& q, cons
   }
   if (a.kind == THZ_Q_SGV1) {
     float dot = 0.f;
-    THZ_FOR_LEVELS(l, a.L) dot += ysave[(size_t)l * n + p] * G * a.lut[l];
+    THZ_FOR_LEVELS(l, a.L) dot += (G * a.lut[l]) * ysave[(size_t)l * n + p];
     float dphase = 0.f;
     THZ_FOR_LEVELS(l, a.L) {
       const float yl = ysave[(size_t)l * n + p];
@@ -420,7 +426,7 @@ __device__ __forceinline__ void quant_bwd_px(const QArgs& a, const QDyn& q, cons
     const bool blend = a.iter_frac <= 0.8f;
     const float gq = blend ? q.beta * G : G;
     float dot = 0.f;
-    THZ_FOR_LEVELS(l, a.L) dot += ysave[(size_t)l * n + p] * gq * a.lut[l];
+    THZ_FOR_LEVELS(l, a.L) dot += (gq * a.lut[l]) * ysave[(size_t)l * n + p];
     const float phase = a.phase_scale * hm;
     float dphase = 0.f;
     THZ_FOR_LEVELS(l, a.L) {
