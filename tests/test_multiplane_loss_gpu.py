@@ -8,10 +8,16 @@ Against the separate path (propagate_planes, then the loss kernel over the Z B p
 batch, times Z): the stored planes bit for bit (same K1 / K2 / K3), the loss within 1e-6 relative
 (one-pass fp64 sums reduced in another order), field / weight gradients within 1e-5 rel-L2.
 Geometries: P = 300 (the dual-plane system, compile-time plan), P = 500 (the extended-DOF system,
-runtime plan, planes from device memory), a plain field with a per-item and a shared target."""
+compile-time 5 4 5 5 plan, planes from device memory), a plain field with a per-item and a shared
+target; and a hypothesis-drawn sweep over sizes (compile-time, power-of-two and runtime plans),
+plane lists, batches and target broadcasts."""
+import os
+
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 from tests.golden_io import rel_l2
 
@@ -44,6 +50,43 @@ def test_plain_field_multiplane_loss_fused_equals_separate(H, ps, Z, B, shared):
     lref = optics.intensity_mse(ref.reshape((Z * B, 1, H, H)), tgt) * float(Z)
     lref.backward()
     assert torch.equal(out.detach(), ref.detach())
+    lv, rv = float(loss.detach()), float(lref.detach())
+    assert abs(lv - rv) <= 1e-6 * abs(rv), (lv, rv)
+    assert rel_l2(xf.grad.cpu().numpy(), xs.grad.cpu().numpy()) <= 1e-5
+
+
+@settings(max_examples=int(os.environ.get("THZ_PROP_EXAMPLES", "40")), deadline=None, database=None,
+          derandomize=os.environ.get("THZ_PROP_RANDOM", "0") != "1",
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(st.fixed_dictionaries({"geo": st.sampled_from([(100, 2), (100, 4), (64, 2), (512, 1), (90, 1), (37, 2)]),
+                              "Z": st.integers(1, 6), "B": st.integers(1, 4), "shared": st.booleans(),
+                              "uniform": st.booleans(), "seed": st.integers(0, 2 ** 31 - 1)}))
+def test_multiplane_loss_fused_equals_separate_drawn(case):
+    """The fused pipeline against the separate one over drawn geometries (P = 300 / 500 compile-time,
+    P = 1024 power of two, runtime plans at P = 128 / 180 / 111), plane counts (Z = 1: the
+    single-item loss finish), batches, shared or per-item targets and uniform (the plane recurrence
+    at P = 1024) or scattered planes: planes bit-identical, loss 1e-6, gradient 1e-5."""
+    from quantizationawarethzdoe_amd import optics, propagation as P
+    dev = _dev()
+    (H, ps), Z, B = case["geo"], case["Z"], case["B"]
+    rng = np.random.default_rng(case["seed"])
+    x = torch.from_numpy((rng.standard_normal((B, 1, H, H)) + 1j * rng.standard_normal((B, 1, H, H)))
+                         .astype(np.complex64)).to(dev)
+    wl, sp = [C0 / 300e9], (1e-3, 1e-3)
+    if case["uniform"]:
+        zs = [float(v) for v in torch.linspace(0.04, 0.04 + 0.005 * (Z - 1), Z, dtype=torch.float32)]
+    else:
+        zs = [float(np.float32(v)) for v in rng.uniform(0.02, 0.2, Z)]
+    ph, pw = P.asm_padding(H, H, (ps, ps))
+    tgt = torch.from_numpy(rng.random((1 if case["shared"] else Z * B, 1, H, H)).astype(np.float32)).to(dev)
+    xf = x.clone().requires_grad_(True)
+    out, loss = P.asm_propagate_loss(xf, tgt, wl, sp, zs, ph, pw)
+    loss.backward()
+    xs = x.clone().requires_grad_(True)
+    ref = P.asm_propagate(xs, wl, sp, zs, ph, pw)
+    lref = optics.intensity_mse(ref.reshape((Z * B, 1, H, H)), tgt) * float(Z)
+    lref.backward()
+    assert torch.equal(out.detach().reshape(ref.shape), ref.detach())
     lv, rv = float(loss.detach()), float(lref.detach())
     assert abs(lv - rv) <= 1e-6 * abs(rv), (lv, rv)
     assert rel_l2(xf.grad.cpu().numpy(), xs.grad.cpu().numpy()) <= 1e-5
