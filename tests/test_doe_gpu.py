@@ -13,10 +13,13 @@ draw (SURVEY.md §8(c) proposes 1e-6; the fp32 phase k (h + b)(n - 1) ~ 12 rad c
 rel-L2 <= 1e-4 (sums over B, C and mirrored / upsampled pixels in a different order).
 """
 import contextlib
+import os
 
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 from oracle import thz_oracle as orc
 from tests.golden_io import arrays, manifest, rel_l2, wavelengths
@@ -305,6 +308,65 @@ def test_fused_modulate_asm_equals_separate(shape, dsize):
     assert rel_l2(o1.numpy(), o2.numpy()) <= 1e-6
     assert rel_l2(gx1.numpy(), gx2.numpy()) <= 1e-6
     assert rel_l2(gw1.numpy(), gw2.numpy()) <= 1e-5
+
+
+FUSED_CLASSES = ["FullPrecisionDOELayer", "SoftGumbelQuantizedDOELayerv3", "STEQuantizedDOELayer",
+                 "PSQuantizedDOELayer", "NaiveGumbelQuantizedDOELayer", "SoftGumbelQuantizedDOELayerv2",
+                 "RotationallySymmetricScoreGumbelSoftQuantizedDOELayer", "RotationallySymmetricPSQuantizedQuantizedDOELayer"]
+
+
+@settings(max_examples=int(os.environ.get("THZ_PROP_EXAMPLES", "40")), deadline=None, database=None,
+          derandomize=os.environ.get("THZ_PROP_RANDOM", "0") != "1",
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(st.fixed_dictionaries({"cls": st.sampled_from(FUSED_CLASSES), "n": st.integers(8, 64), "up": st.sampled_from([1, 2]),
+                              "B": st.integers(1, 3), "C": st.integers(1, 2), "s": st.sampled_from([1, 2]),
+                              "L": st.integers(2, 8), "frac": st.floats(0.0, 0.99), "z": st.floats(0.02, 0.3),
+                              "seed": st.integers(0, 2 ** 31 - 1)}))
+def test_fused_modulate_asm_equals_separate_drawn(case):
+    """test_fused_modulate_asm_equals_separate over drawn layer classes, DOE sizes (the field 1 or 2
+    x the map: nearest upsampling), levels, schedule positions, batches, wavelengths, paddings and
+    distances: the DOE layer's pending modulation applied in the ASM row pass (with the one-kernel
+    layer backward where the map has the field's size) against the modulate kernel first -- height
+    maps bit-identical, outputs 1e-6, field and weight gradients 1e-5 rel-L2."""
+    from quantizationawarethzdoe_amd.Components import QuantizedDOE as Q
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    dev = _dev()
+    cls, n, up = case["cls"], case["n"], case["up"]
+    B, C, H = case["B"], case["C"], n * up
+    psq = "PSQ" in cls
+    optim = {"c_s": 100, "tau_max": 20 if psq else 2.5, "tau_min": 1 if psq else 1.5}
+    dp = {'doe_size': [n, n], 'doe_dxy': 1e-3 * up, 'doe_level': case["L"], 'look_up_table': None, 'num_unit': None,
+          'height_constraint_max': 1e-3, 'tolerance': 1e-5, 'material': [2.66, 0.03]}
+    torch.manual_seed(case["seed"] % 1000)
+    layer = getattr(Q, cls)(dp, device=dev) if "FullPrecision" in cls else getattr(Q, cls)(dp, optim, device=dev)
+    param = next(iter(layer.parameters()))
+    asm = ASM_prop(z_distance=case["z"], padding_scale=case["s"], device=dev)
+    g = torch.Generator().manual_seed(case["seed"])
+    with torch.no_grad():
+        param.copy_(torch.randn(param.shape, generator=g) * 2)
+    x = torch.randn((B, C, H, H), dtype=torch.complex64, generator=g).to(dev)
+    gout = torch.randn((B, C, H, H), dtype=torch.complex64, generator=g).to(dev)
+    wl = [2.998e8 / 300e9, 2.998e8 / 250e9][:C]
+    frac = None if cls.endswith(("FullPrecisionDOELayer", "STEQuantizedDOELayer")) else case["frac"]
+    res = []
+    for fused in (True, False):
+        xd = x.clone().requires_grad_(True)
+        param.grad = None
+        torch.manual_seed(7)
+        f = layer(ElectricField(xd, wavelengths=wl if C > 1 else wl[0], spacing=1e-3, device=dev), frac)
+        if not fused:
+            _ = f.data  # form the modulated field with the modulate kernel
+        out = asm(f).data
+        out.backward(gout)
+        res.append((out.detach().cpu(), xd.grad.cpu(), param.grad.detach().cpu().clone(),
+                    layer.height_map.detach().cpu().clone()))
+    (o1, gx1, gw1, h1), (o2, gx2, gw2, h2) = res
+    assert torch.equal(h1, h2)
+    assert rel_l2(o1.numpy(), o2.numpy()) <= 1e-6
+    assert rel_l2(gx1.numpy(), gx2.numpy()) <= 1e-6
+    if float(gw2.abs().max()) > 0:
+        assert rel_l2(gw1.numpy(), gw2.numpy()) <= 1e-5
 
 
 @pytest.mark.parametrize("L", [3, 8, 16])
