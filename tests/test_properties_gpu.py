@@ -268,7 +268,7 @@ def test_czt_overlap_add_linearity_and_adjoint(case):
     gx, = torch.autograd.grad(out, xg, grad_outputs=g)
     lhs = torch.vdot(out.detach().reshape(-1).to(torch.complex128), g.reshape(-1).to(torch.complex128))
     rhs = torch.vdot(x.reshape(-1).to(torch.complex128), gx.reshape(-1).to(torch.complex128))
-    scale = max(float(out.norm()) * float(g.norm()), float(x.norm()) * float(gx.norm()))
+    scale = max(float(out.detach().norm()) * float(g.norm()), float(x.norm()) * float(gx.norm()))
     assert abs(complex(lhs - rhs)) <= 1e-5 * scale, (abs(complex(lhs - rhs)), scale)
 
 
