@@ -8,9 +8,13 @@ whole step is checked against the same composition of oracle pieces on the host:
 loss within 1e-4 relative, weight gradients within 1e-3 rel-L2 (four fp32 ASM propagations and
 their adjoints on each side, reductions in a different order).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 from tests.golden_io import rel_l2
 
@@ -76,6 +80,44 @@ def test_donn_step_loss_and_grads_vs_oracle(chained, B):
         gp = next(iter(d.parameters())).grad
         if not chained and i < 2:
             assert gp is None or float(gp.abs().max()) == 0.0  # the notebook discards these branches
+            continue
+        assert rel_l2(gp.cpu().numpy(), wo[i].grad.numpy()) <= 1e-3
+
+
+@settings(max_examples=int(os.environ.get("THZ_PROP_EXAMPLES", "12")), deadline=None, database=None,
+          derandomize=os.environ.get("THZ_PROP_RANDOM", "0") != "1",
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(st.fixed_dictionaries({"B": st.integers(1, 48), "chained": st.booleans(), "seed": st.integers(0, 2 ** 31 - 1)}))
+def test_donn_step_drawn_batches_vs_oracle(case):
+    """test_donn_step_loss_and_grads_vs_oracle over drawn batch sizes -- odd ones and ones that do
+    not fill the modulate backward's 16 batch lanes -- in both semantics."""
+    from quantizationawarethzdoe_amd import donn
+    B, chained = case["B"], case["chained"]
+    g = torch.Generator().manual_seed(case["seed"])
+    u = torch.rand(B, 1, 100, 100, generator=g)
+    labels = torch.randint(0, 10, (B,), generator=g)
+    noises = [torch.rand(100, 100, generator=g) for _ in range(3)]
+    torch.manual_seed(case["seed"] % 1000)
+    model = donn.DONN(device=_dev())
+    ws = [next(iter(d.parameters())).detach().cpu().clone() for d in model.does]
+    targets = donn.detector_targets(device=_dev())
+    tr = donn.DONNTrainer(model, targets, chained=chained)
+    it = iter(noises)
+    orig = torch.rand_like
+    torch.rand_like = lambda t, *a, **k: next(it).to(device=t.device, dtype=t.dtype)
+    try:
+        loss = tr._loss(u.to(_dev()), targets.index_select(0, labels.to(_dev())), None)
+        loss.backward()
+    finally:
+        torch.rand_like = orig
+    wo = [w.clone().requires_grad_(True) for w in ws]
+    lo = _oracle_loss(wo, u, targets.cpu().index_select(0, labels), noises, chained)
+    lo.backward()
+    assert abs(float(loss.detach()) - float(lo.detach())) <= 1e-4 * float(lo.detach())
+    for i, d in enumerate(model.does):
+        gp = next(iter(d.parameters())).grad
+        if not chained and i < 2:
+            assert gp is None or float(gp.abs().max()) == 0.0
             continue
         assert rel_l2(gp.cpu().numpy(), wo[i].grad.numpy()) <= 1e-3
 
