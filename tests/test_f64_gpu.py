@@ -11,9 +11,13 @@ reference's operation order; measured ~1e-14), <= 1e-8 for CZT (the reference's 
 complex pow W^(j^2/2) in fp64, this build's cis(theta j^2/2): the phases agree to ~1e-10
 relative at these lengths).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, example, given, settings
+from hypothesis import strategies as st
 
 from tests.golden_io import arrays, manifest, rel_l2
 
@@ -160,3 +164,41 @@ def test_fft64_rows_vs_numpy(n):
     xt = torch.from_numpy(x).to(_dev())
     assert rel_l2(fft_rows(xt).cpu().numpy(), np.fft.fft(x, axis=-1)) <= 1e-13
     assert rel_l2(fft_rows(xt, inverse=True).cpu().numpy(), np.fft.ifft(x, axis=-1) * n) <= 1e-13
+
+
+@settings(max_examples=int(os.environ.get("THZ_PROP_EXAMPLES", "15")), deadline=None, database=None,
+          derandomize=os.environ.get("THZ_PROP_RANDOM", "0") != "1",
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.data_too_large])
+@given(st.fixed_dictionaries({"H": st.integers(1, 900), "W": st.integers(1, 900), "C": st.integers(1, 2),
+                              "s": st.sampled_from([1, 1.5, 2]), "z": st.floats(0.01, 0.5),
+                              "bl": st.sampled_from(["exact", "approx", "none"]), "f": st.floats(220.0, 380.0),
+                              "dx": st.sampled_from([0.5, 1.0]), "seed": st.integers(0, 2 ** 31 - 1)}))
+# large prime factors in the padded lengths (2 x 853, 3 x 641): the table-DFT stage
+@example({"H": 899, "W": 853, "C": 1, "s": 1, "z": 0.1, "bl": "exact", "f": 300.0, "dx": 0.5, "seed": 1})
+@example({"H": 700, "W": 641, "C": 2, "s": 2, "z": 0.3, "bl": "approx", "f": 250.0, "dx": 1.0, "seed": 2})
+def test_asm_f64_drawn_sizes_vs_oracle(case):
+    """The fp64 ASM at drawn sizes up to P = 2700 (runtime mixed-radix plans: radix 4, 2, 3, 5, 7 in
+    registers, any other prime factor by a table DFT) against the fp64 oracle, rel-L2 <= 1e-10, and
+    its backward the adjoint to 1e-12."""
+    from oracle import thz_oracle as orc
+    from quantizationawarethzdoe_amd.DataType.ElectricField import ElectricField
+    from quantizationawarethzdoe_amd.Props.ASM_Prop import ASM_prop
+    rng = np.random.default_rng(case["seed"])
+    H, W, C = case["H"], case["W"], case["C"]
+    lam = _wl64([case["f"] + 37 * c for c in range(C)])
+    x = torch.from_numpy(rng.standard_normal((1, C, H, W)) + 1j * rng.standard_normal((1, C, H, W))).to(_dev())
+    prop = ASM_prop(z_distance=case["z"], padding_scale=case["s"], bandlimit_kernel=case["bl"] != "none",
+                    bandlimit_type="exact" if case["bl"] == "none" else case["bl"], device=_dev())
+    xg = x.clone().requires_grad_(True)
+    out = prop(ElectricField(xg, wavelengths=lam, spacing=case["dx"] * 1e-3, device=_dev())).data
+    assert out.dtype == torch.complex128
+    sp = torch.tensor([case["dx"] * 1e-3] * 2, dtype=torch.float32).double()
+    kw = dict(bandlimit=case["bl"] != "none", bandlimit_type="exact" if case["bl"] == "none" else case["bl"])
+    ref = orc.asm_forward(x.cpu(), lam, sp, case["z"], case["s"], **kw)
+    e = float((out.detach().cpu() - ref).norm() / ref.norm())
+    assert e <= 1e-10, e
+    g = torch.from_numpy(rng.standard_normal(tuple(out.shape)) + 1j * rng.standard_normal(tuple(out.shape))).to(_dev())
+    gx, = torch.autograd.grad(out, xg, grad_outputs=g)
+    lhs = torch.vdot(out.detach().reshape(-1), g.reshape(-1))
+    rhs = torch.vdot(x.reshape(-1), gx.reshape(-1))
+    assert abs(complex(lhs - rhs)) <= 1e-12 * float(out.detach().norm()) * float(g.norm())
