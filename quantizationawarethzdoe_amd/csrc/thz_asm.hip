@@ -579,9 +579,18 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             if (r >= 4 && r < 12) continue;
-            const float2 g = cmul(sp[0][r], sp[0][rec_dslot(r)]);
-            const float th = eps * sq[0][r];
-            sp[0][r] = make_float2(fmaf(-th, g.y, g.x), fmaf(th, g.x, g.y));
+            sp[0][r] = cmul(sp[0][r], sp[0][rec_dslot(r)]);
+          }
+          // the step correction 1 + i eps sq, skipped on a scalar branch where the step is dz
+          // exactly (60 of cfg2's 63 steps), where it would leave every value as it is
+          if (__builtin_amdgcn_readfirstlane(__float_as_int(eps)) != 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              if (r >= 4 && r < 12) continue;
+              const float2 g = sp[0][r];
+              const float th = eps * sq[0][r];
+              sp[0][r] = make_float2(fmaf(-th, g.y, g.x), fmaf(th, g.x, g.y));
+            }
           }
         }
         zprev = z;
