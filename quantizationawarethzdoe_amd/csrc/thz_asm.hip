@@ -491,7 +491,9 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         int mmax = -1, ok = 1;
         for (int q = 0; q < z_hi - z_lo; ++q) {
           mmax = max(mmax, mz[q]);
-          ok &= zok[q];
+          // the band may only narrow over the chunk (cfg2's increasing z): an element that leaves
+          // it is zeroed in the recurrence for good (below)
+          ok &= zok[q] && (q == 0 || mz[q] <= mz[q - 1]);
         }
         rec = __builtin_amdgcn_readfirstlane(ok) && __builtin_amdgcn_readfirstlane(mmax) < PN / 4;
       }
@@ -550,6 +552,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     // structurizer kept one form's live-ins live through the other and spilled).
     constexpr bool REC = !ZSUM && RL == 16 && MBL == 1;
     float dz = 0.f, zprev = 0.f;
+    int Mprev = -2;  // below every band value (M = -1: no row of the column kept)
     if constexpr (REC) {
       if (rec) {
         const float z0 = zval(a, a.zoff + z_lo);
@@ -597,21 +600,33 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       }
       int tz = threadIdx.x;
       asm volatile("" : "+v"(tz));
+      const int Ms = __builtin_amdgcn_readfirstlane(M);
+      if constexpr (REC) {
+        // the band's edge: on the chunk's first plane and wherever the band narrows (a few of
+        // cfg2's planes), the elements outside it are zeroed in G itself -- they stay zero through
+        // the recurrence's products, and the band never widens again (the eligibility above) --
+        // so the loads below need no per-plane mask
+        if (rec && Ms != Mprev) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            if (r >= 4 && r < 12) continue;
+            // element tz + r PN/16: m_x = tz + r PN/16 (r < 4), tz + r PN/16 - PN (r >= 12)
+            const bool keep = r < 4 ? tz <= Ms - r * (PN / 16) : tz >= PN - r * (PN / 16) - Ms;
+            if (!keep) sp[0][r] = make_float2(0.f, 0.f);
+          }
+        }
+        Mprev = Ms;
+      }
       // the inverse's first stage (radix RL, L = 1) reads exactly the elements this thread
       // holds in sp: multiply by H_z on the fly in the loader
       // the first stage's operands r in [4, 12) are the rows PN/4 <= |m_x| < 3 PN/4: when this
       // plane's kept band M is below PN/4 (all but the few columns near m_y = 0 at cfg2) they are
       // zero for every thread, and a scalar branch skips their sincos and product
-      const int Ms = __builtin_amdgcn_readfirstlane(M);
       const bool mid0 = Ms < PN / 4;
       auto ld1 = [&](int m, int r, int idx) {
         if (RL == 16 && r >= 4 && r < 12 && mid0) return make_float2(0.f, 0.f);
         if constexpr (REC) {
-          if (rec) {
-            // element tz + r PN/16: m_x = tz + r PN/16 (r < 4), tz + r PN/16 - PN (r >= 12)
-            const bool keep = r < 4 ? tz <= Ms - r * (PN / 16) : tz >= PN - r * (PN / 16) - Ms;
-            return keep ? sp[0][r] : make_float2(0.f, 0.f);
-          }
+          if (rec) return sp[0][r];  // out-of-band elements already zero (above)
         }
         const int mx = freq_index(idx, PN);
         if (mx > M || -mx > M) return make_float2(0.f, 0.f);

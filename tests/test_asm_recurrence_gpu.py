@@ -57,9 +57,14 @@ def test_recurrence_vs_sincos_and_oracle(zs):
     x, lam, sp = _narrow_input(1024, 3)
     a = _run(x, lam, sp, zs, 512, True)
     b = _run(x, lam, sp, zs, 512, False)
-    # the two forms really differ (the recurrence ran) except on the first plane
     assert torch.equal(a[0], b[0])
-    assert not torch.equal(a, b)
+    if zs[-1] < zs[0]:
+        # a decreasing sweep widens the band from plane to plane: the recurrence (which zeroes the
+        # elements leaving a narrowing band in place) is not taken, every plane is the sincos form's
+        assert torch.equal(a, b)
+    else:
+        # the two forms really differ (the recurrence ran) except on the first plane
+        assert not torch.equal(a, b)
     for k in range(len(zs)):
         assert rel_l2(a[k].cpu().numpy(), b[k].cpu().numpy()) <= 2e-5, k
     check = sorted({0, 1, len(zs) // 2, len(zs) - 1})
