@@ -361,18 +361,18 @@ __global__ void __launch_bounds__(1024) THZ_ROW_ATTR asm_rows_fwd(const float2* 
 // ---------------------------------------------------------------------------------------------
 // K2: per band column: FFT(Ph) once, then per z: x H_z, IFFT(Ph), crop, scale -> U[z][bc][c][r]
 // ---------------------------------------------------------------------------------------------
-// Plane zz (> 0) of the column task's range [z_lo, z_hi) may be reached by the plane recurrence of
-// asm_cols_body: with dz = z_1 - z_0 of the range, the step z_zz - z_{zz-1} and eps = step - dz are
-// both EXACT fp32 differences (so the recurrence's phase sums to (z_zz - z_0) sq exactly) and
-// |eps| k <= 1e-4 rad (so 1 + i eps sq stands for exp(i eps sq) to 5e-9).  Evaluated on the device,
-// so a device-resident plane list (thz_asm_desc.z_dev) decides exactly as the same host list does.
+// Plane zz of the column task's range [z_lo, z_hi) may be reached from its predecessor in the order
+// the planes are run (ascending, or descending from the range's last plane) by the plane recurrence
+// of asm_cols_body: with dz the range's first step in that order, the step to zz and eps = step - dz
+// are both EXACT fp32 differences (so the recurrence's phase sums to (z_zz - z_first) sq exactly)
+// and |eps| k <= 1e-4 rad (so 1 + i eps sq stands for exp(i eps sq) to 5e-9).  Evaluated on the
+// device, so a device-resident plane list (thz_asm_desc.z_dev) decides exactly as the host list does.
 // register slot of the step factor D of kept spectrum value r (r < 4 or r >= 12): the slots
 // [4, 12) of sp, whose values are zero whenever the recurrence runs
 __host__ __device__ constexpr int rec_dslot(int r) { return r < 4 ? r + 4 : r - 4; }
 
-__device__ __forceinline__ bool recurrence_step_ok(const AsmArgs& a, int z_lo, int zz, float kl) {
-  const float z0 = zval(a, a.zoff + z_lo), z1 = zval(a, a.zoff + z_lo + 1);
-  const float zp = zval(a, a.zoff + z_lo + zz - 1), zc = zval(a, a.zoff + z_lo + zz);
+// the step from plane zp to plane zc against the range's first step z0 -> z1 (either direction)
+__device__ __forceinline__ bool recurrence_step_ok(float z0, float z1, float zp, float zc, float kl) {
   const float dz = z1 - z0, step = zc - zp, eps = step - dz;
   return dz != 0.0f && (double)dz == (double)z1 - (double)z0 && (double)step == (double)zc - (double)zp &&
          (double)eps == (double)step - (double)dz && fabs((double)eps) * (double)kl <= 1e-4;
@@ -471,7 +471,18 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         }
       }
       mz[zz] = lo;
-      if constexpr (!ZSUM) zok[zz] = zz == 0 || recurrence_step_ok(a, z_lo, zz, kl);
+      if constexpr (!ZSUM) {
+        // bit 0: plane zz is reached from zz - 1 in ascending order; bit 1: from zz + 1 in
+        // descending order (the range's last plane first)
+        const int nzr = z_hi - z_lo;
+        auto zv = [&](int q) { return zval(a, a.zoff + z_lo + q); };
+        const bool fwd = zz == 0 || (nzr >= 2 && recurrence_step_ok(zv(0), zv(1), zv(zz - 1), zv(zz), kl));
+        const bool bwd = zz == nzr - 1 ||
+                         (nzr >= 2 && recurrence_step_ok(zv(nzr - 1), zv(nzr - 2), zv(zz + 1), zv(zz), kl));
+        // bit 2 (on plane 0): |z| falls along the range (a sweep towards the aperture)
+        const bool inward = zz == 0 && fabsf(zv(nzr - 1)) < fabsf(zv(0));
+        zok[zz] = (fwd ? 1 : 0) | (bwd ? 2 : 0) | (inward ? 4 : 0);
+      }
     }
     // sqrt(k^2 - Kx^2 - Ky^2) of the elements this thread holds: z-independent, computed once
     // per column (the per-z work is then one product and one sincos per element)
@@ -485,17 +496,25 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
       }
     __syncthreads();  // mz visible
     // the plane recurrence (below) for this column?
-    bool rec = false;
+    bool rec = false, rev = false;
     if constexpr (!ZSUM && RL == 16 && MBL == 1) {
       if (a.zrec && z_hi - z_lo >= 3) {
-        int mmax = -1, ok = 1;
+        int mmax = -1, okf = 1, okr = 1;
         for (int q = 0; q < z_hi - z_lo; ++q) {
           mmax = max(mmax, mz[q]);
-          // the band may only narrow over the chunk (cfg2's increasing z): an element that leaves
-          // it is zeroed in the recurrence for good (below)
-          ok &= zok[q] && (q == 0 || mz[q] <= mz[q - 1]);
+          // the band may only narrow in the order the planes are run (an element that leaves it
+          // is zeroed in the recurrence for good, below): ascending order for a band that narrows
+          // with the plane index (cfg2's increasing z), descending order for one that widens
+          // (a decreasing z-sweep)
+          okf &= (zok[q] & 1) && (q == 0 || mz[q] <= mz[q - 1]);
+          okr &= (zok[q] & 2) && (q == 0 || mz[q] >= mz[q - 1]);
         }
-        rec = __builtin_amdgcn_readfirstlane(ok) && __builtin_amdgcn_readfirstlane(mmax) < PN / 4;
+        okf = __builtin_amdgcn_readfirstlane(okf);
+        okr = __builtin_amdgcn_readfirstlane(okr);
+        rec = (okf || okr) && __builtin_amdgcn_readfirstlane(mmax) < PN / 4;
+        // a band constant over the range allows both orders: run the range from its plane nearest
+        // the aperture, as every column with a changing band of the same sweep does
+        rev = rec && okr && (!okf || (zok[0] & 4));
       }
     }
     if constexpr (ZSUM) {
@@ -544,7 +563,9 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     // which tracks the given fp32 planes exactly: recurrence_step_ok has checked that every
     // difference is exact in fp32 and |eps_j| k <= 1e-4 rad, so 1 + i theta stands for
     // exp(i theta) to 5e-9.  D is formed in double and rounded once (<= 6e-8 per plane, 4e-6
-    // over 64 planes); the chunk's first plane is the sincos form's value bit for bit.
+    // over 64 planes); the first plane run is the sincos form's value bit for bit.  The planes
+    // run in the order in which the column's band narrows (ascending z for cfg2; a decreasing
+    // sweep runs from the range's last plane), so no element ever re-enters the band.
     // Taken when the column keeps no row with |m_x| >= PN/4 on any plane of the chunk: the
     // inverse's first-stage operands r in [4, 12) are then zero, and the registers of those 8
     // spectrum values hold the 8 step factors D (sp[0][rec_dslot(r)]); sq holds +-sq.  Both forms
@@ -553,10 +574,12 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     constexpr bool REC = !ZSUM && RL == 16 && MBL == 1;
     float dz = 0.f, zprev = 0.f;
     int Mprev = -2;  // below every band value (M = -1: no row of the column kept)
+    // plane order: ascending, or descending where the recurrence runs the range backwards
+    const int zfirst = rev ? z_hi - 1 : z_lo, zstep = rev ? -1 : 1;
     if constexpr (REC) {
       if (rec) {
-        const float z0 = zval(a, a.zoff + z_lo);
-        dz = zval(a, a.zoff + z_lo + 1) - z0;
+        const float z0 = zval(a, a.zoff + zfirst);
+        dz = zval(a, a.zoff + zfirst + zstep) - z0;
         zprev = z0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -573,11 +596,12 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
         }
       }
     }
-    for (int zz = z_lo; zz < z_hi; ++zz) {
+    for (int it = 0; it < z_hi - z_lo; ++it) {
+      const int zz = zfirst + it * zstep;
       const float z = zval(a, a.zoff + zz);
       const int M = mz[zz - z_lo];
       if constexpr (REC) {
-        if (rec && zz > z_lo) {
+        if (rec && it > 0) {
           const float eps = tf_sub(tf_sub(z, zprev), dz);
 #pragma unroll
           for (int r = 0; r < 16; ++r) {

@@ -7,7 +7,9 @@ Tolerances: each plane vs the fp64 oracle <= max(1e-4, 1.5 x the fp32 oracle's o
 (tests/test_asm_gpu.py's rule), and vs the per-plane sincos form of the same kernel (the
 THZ_K2_RECURRENCE=0 switch) <= 2e-5 rel-L2: the recurrence's phase error is <= 4e-6 rad after 64
 planes (D rounded once to fp32, 6e-8 per plane) against the sincos form's fp32 rounding of z sq
-(<= 3e-5 rad at z sq ~ 750 rad).  The chunk's first plane is bit-identical in both forms.
+(<= 3e-5 rad at z sq ~ 750 rad).  The first plane the recurrence runs is bit-identical in both
+forms: the chunk's first plane for an increasing sweep (the band narrows with z), its last plane for
+a decreasing one (run backwards, so the band still only narrows).
 """
 import os
 
@@ -57,14 +59,11 @@ def test_recurrence_vs_sincos_and_oracle(zs):
     x, lam, sp = _narrow_input(1024, 3)
     a = _run(x, lam, sp, zs, 512, True)
     b = _run(x, lam, sp, zs, 512, False)
-    assert torch.equal(a[0], b[0])
-    if zs[-1] < zs[0]:
-        # a decreasing sweep widens the band from plane to plane: the recurrence (which zeroes the
-        # elements leaving a narrowing band in place) is not taken, every plane is the sincos form's
-        assert torch.equal(a, b)
-    else:
-        # the two forms really differ (the recurrence ran) except on the first plane
-        assert not torch.equal(a, b)
+    # the recurrence's first plane: the sweep's nearest plane (where the band is widest)
+    first = 0 if zs[-1] > zs[0] else len(zs) - 1
+    assert torch.equal(a[first], b[first])
+    # the two forms really differ elsewhere (the recurrence ran)
+    assert not torch.equal(a, b)
     for k in range(len(zs)):
         assert rel_l2(a[k].cpu().numpy(), b[k].cpu().numpy()) <= 2e-5, k
     check = sorted({0, 1, len(zs) // 2, len(zs) - 1})
@@ -80,16 +79,21 @@ def test_recurrence_vs_sincos_and_oracle(zs):
         assert e <= max(1e-4, 1.5 * floor), (k, zs[k], e, floor)
 
 
-def test_recurrence_split_chunks_and_kparts():
+@pytest.mark.parametrize("order", ["increasing", "decreasing"])
+def test_recurrence_split_chunks_and_kparts(order):
     """40 planes in z-chunks of 16 (two full chunks and a tail of 8): each chunk restarts the
-    recurrence from its own first plane, and the last dispatch round's columns split into z-ranges
-    (kparts) restart it from each range's first plane."""
+    recurrence from its own first plane in run order (its first plane, or its last for a decreasing
+    sweep), and the last dispatch round's columns split into z-ranges (kparts) restart it from each
+    range's own."""
     x, lam, sp = _narrow_input(1024, 4)
     zs = [float(v) for v in torch.linspace(30e-3, 90e-3, 40, dtype=torch.float64)]
+    if order == "decreasing":
+        zs = zs[::-1]
     a = _run(x, lam, sp, zs, 512, True, z_chunk=16)
     b = _run(x, lam, sp, zs, 512, False, z_chunk=16)
-    for k in (0, 16, 32):
+    for k in ((0, 16, 32) if order == "increasing" else (15, 31, 39)):
         assert torch.equal(a[k], b[k]), k
+    assert not torch.equal(a, b)
     for k in range(40):
         assert rel_l2(a[k].cpu().numpy(), b[k].cpu().numpy()) <= 2e-5, k
 

@@ -165,7 +165,9 @@ def test_asm_uniform_sweep_matches_single_planes(case):
     the column pass may advance the planes by the plane recurrence (csrc/thz_asm.hip
     recurrence_step_ok; taken per column when every step is an exact fp32 difference and the band
     stays under P/4), against each plane propagated on its own (one plane: the per-plane sincos):
-    fp32 rel-L2 <= max(2e-5, ulp(k |z|) / 2) per plane, the first plane bit-identical.  (2e-5 is
+    fp32 rel-L2 <= max(2e-5, ulp(k |z|) / 2) per plane; where |z| grows along the sweep the first
+    plane is bit-identical (the recurrence starts there; a sweep towards the aperture runs its
+    columns from the far end, so its bands still only narrow).  (2e-5 is
     tests/test_asm_recurrence_gpu.py's bound at cfg2's phases; the per-plane sincos form rounds its
     phase z sq <= k |z| to fp32 -- up to half an ulp per element, 3.6e-5 / 4.3e-5 rel-L2 at k z =
     1.9e3 / 1.3e3 rad (ulp 1.2e-4) in wide random sweeps -- while the recurrence carries the phase
@@ -180,9 +182,10 @@ def test_asm_uniform_sweep_matches_single_planes(case):
     sp = [float(np.float32(case["dx"] * 1e-3))] * 2
     x = _rand(rng, (1, 1, H, W), torch.complex64)
     multi = asm_apply(x, lam, sp, zs, ph, pw, True, 1)
+    outward = all(abs(zs[k + 1]) >= abs(zs[k]) for k in range(Z - 1))
     for k, z in enumerate(zs):
         one = asm_apply(x, lam, sp, [z], ph, pw, True, 1)[0]
-        if k == 0:
+        if k == 0 and outward:
             assert torch.equal(multi[0], one)
         else:
             e = float((multi[k] - one).norm() / one.norm())
