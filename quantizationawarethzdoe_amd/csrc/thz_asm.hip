@@ -499,22 +499,34 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     bool rec = false, rev = false;
     if constexpr (!ZSUM && RL == 16 && MBL == 1) {
       if (a.zrec && z_hi - z_lo >= 3) {
-        int mmax = -1, okf = 1, okr = 1;
-        for (int q = 0; q < z_hi - z_lo; ++q) {
-          mmax = max(mmax, mz[q]);
-          // the band may only narrow in the order the planes are run (an element that leaves it
-          // is zeroed in the recurrence for good, below): ascending order for a band that narrows
-          // with the plane index (cfg2's increasing z), descending order for one that widens
-          // (a decreasing z-sweep)
-          okf &= (zok[q] & 1) && (q == 0 || mz[q] <= mz[q - 1]);
-          okr &= (zok[q] & 2) && (q == 0 || mz[q] >= mz[q - 1]);
+        // one plane per lane, every wave voting on its own copy (no loop over the planes per
+        // thread, no extra barrier); the votes are wave-uniform
+        bool okf = true, okr = true, wide = false;
+        const int lane = threadIdx.x & 63;
+        for (int q0 = 0; q0 < z_hi - z_lo; q0 += 64) {
+          const int q = q0 + lane;
+          bool pf = true, pr = true, pw = false;
+          if (q < z_hi - z_lo) {
+            // the band may only narrow in the order the planes are run (an element that leaves
+            // it is zeroed in the recurrence for good, below): ascending order for a band that
+            // narrows with the plane index (cfg2's increasing z), descending order for one that
+            // widens (a decreasing z-sweep)
+            const int m = mz[q], mp = q > 0 ? mz[q - 1] : m, zk = zok[q];
+            pf = (zk & 1) && m <= mp;
+            pr = (zk & 2) && m >= mp;
+            pw = m >= PN / 4;
+          }
+          okf = okf && __ballot(!pf) == 0;
+          okr = okr && __ballot(!pr) == 0;
+          wide = wide || __ballot(pw) != 0;
         }
-        okf = __builtin_amdgcn_readfirstlane(okf);
-        okr = __builtin_amdgcn_readfirstlane(okr);
-        rec = (okf || okr) && __builtin_amdgcn_readfirstlane(mmax) < PN / 4;
+        rec = (okf || okr) && !wide;
         // a band constant over the range allows both orders: run the range from its plane nearest
         // the aperture, as every column with a changing band of the same sweep does
-        rev = rec && okr && (!okf || (zok[0] & 4));
+        // (read wave-uniform: the plane order, and with it every plane index and z of the loop
+        // below, stays in scalar registers)
+        const int zk0 = __builtin_amdgcn_readfirstlane(zok[0]);
+        rev = rec && okr && (!okf || (zk0 & 4));
       }
     }
     if constexpr (ZSUM) {
