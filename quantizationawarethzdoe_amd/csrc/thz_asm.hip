@@ -457,8 +457,13 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     const float Ky2 = tf_mul(Ky, Ky);
     // strided over the chunk: a z_chunk may exceed the workgroup (64 threads at P = 1024)
     int* zok = mz + THZ_MAX_Z;  // plane recurrence allowed at this plane (below)
+    // the chunk's z values, staged next to mz for the z-loop of the forward (an LDS read per
+    // plane instead of a dependent global load at the top of every plane)
+    float* zl = reinterpret_cast<float*>(zok + THZ_MAX_Z);
     for (int zz = tid; zz < z_hi - z_lo; zz += nt) {
-      const TfScalars s = tf_scalars(a, lam, zval(a, a.zoff + z_lo + zz));
+      const float zq = zval(a, a.zoff + z_lo + zz);
+      if constexpr (!ZSUM) zl[zz] = zq;
+      const TfScalars s = tf_scalars(a, lam, zq);
       int lo = -1, hi = PN / 2 + 1;
       const int bl = a.bl, P = a.Ph;
       const float dx = a.dx;
@@ -590,8 +595,8 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     const int zfirst = rev ? z_hi - 1 : z_lo, zstep = rev ? -1 : 1;
     if constexpr (REC) {
       if (rec) {
-        const float z0 = zval(a, a.zoff + zfirst);
-        dz = zval(a, a.zoff + zfirst + zstep) - z0;
+        const float z0 = zl[zfirst - z_lo];
+        dz = zl[zfirst + zstep - z_lo] - z0;
         zprev = z0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -610,7 +615,7 @@ __device__ __forceinline__ void asm_cols_body(const float2* __restrict__ T, floa
     }
     for (int it = 0; it < z_hi - z_lo; ++it) {
       const int zz = zfirst + it * zstep;
-      const float z = zval(a, a.zoff + zz);
+      const float z = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(zl[zz - z_lo])));
       const int M = mz[zz - z_lo];
       if constexpr (REC) {
         if (rec && it > 0) {
@@ -1312,7 +1317,7 @@ static int ensure_lds_attr() {
   static std::once_flag once;
   static hipError_t err = hipSuccess;
   std::call_once(once, [] {
-    const int mx = (int)fft_lds_bytes(FFT_MAX_N) + 8 * THZ_MAX_Z;
+    const int mx = (int)fft_lds_bytes(FFT_MAX_N) + 12 * THZ_MAX_Z;
     std::vector<const void*> ks;
     add_kernels<0>(ks);
     add_kernels<1024>(ks);
@@ -1531,7 +1536,7 @@ static int run_pipeline(AsmArgs a, const AsmGeom& g, int Z, const void* in, void
         else
           THZ_MX_COLS(g.Ph, asm_cols_mx, dim3(ntask), dim3(mx_threads(g.Ph)), lds2, s, (const float2*)T, U, ph, a);
       } else {
-        const size_t lds2 = fft_lds_bytes(g.Ph) + 8 * THZ_MAX_Z;  // mz and zok
+        const size_t lds2 = fft_lds_bytes(g.Ph) + 12 * THZ_MAX_Z;  // mz, zok and the z values
         const int ntask = k2_tasks(g, &a, th, lds2);
         a.zrec = !plane_recurrence_disabled();
         THZ_POW2_SWITCH(g.Ph, asm_cols, dim3(ntask), dim3(th), lds2, s, (const float2*)T, U, ph, a);
